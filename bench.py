@@ -1,0 +1,169 @@
+"""bench.py — decode tokens/s of the BLOOM stage pipeline on MI355X (BASELINE.json metric).
+
+N=1 (default): BASELINE.json configs[1] — bloom-1b1 as one stage on one GPU, batch 1,
+512-token prefill (timed separately, reported under "prefill"), then W untimed and K timed
+decode steps.  One "step" = one decode token for every row of the batch through the whole
+model.  N>1 (torchrun, one rank per GPU): the same model split into N stages by the server's
+round-robin layer assignment (server.py:893-905), activations over RCCL send/recv, N rows in
+flight (one per stage) — see distributed_inference_demo_amd/pipeline.py.
+
+Prints ONE JSON line (rank 0).  Inputs are resident in HBM before the timed region.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E vendor peak (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA vendor peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=128)
+    p.add_argument("--warmup", type=int, default=8)
+    p.add_argument("--model", default="bloom-1b1")
+    p.add_argument("--batch", type=int, default=1)
+    p.add_argument("--prompt", type=int, default=512)
+    p.add_argument("--dtype", default="bf16")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU checker on a bounded sample")
+    p.add_argument("--cpu-steps", type=int, default=12)
+    p.add_argument("--no-profile", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(model, steps, seed):
+    """The oracle (C fp32 restatement, OpenMP over the host cores) timed on a bounded sample:
+    KV-cached decode of `steps` tokens after a 16-token prompt, same model, same generator."""
+    import numpy as np
+    from oracle.oracle import OracleStage, num_threads, prompt_ids
+    t0 = time.perf_counter()
+    st = OracleStage(model.hidden, model.n_head, model.n_layer, model.vocab, 0, model.n_layer, bf16=False,
+                     max_batch=1, max_ctx=16 + steps + 8, seed=seed)
+    t_init = time.perf_counter() - t0
+    ids = prompt_ids(1234, 1, 16, model.vocab)
+    tok = st.forward(ids, 1, 16)
+    for i in range(2):  # warm-up tokens
+        tok = st.forward(tok.reshape(1, 1), 1, 1, past_len=16 + i)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        tok = st.forward(tok.reshape(1, 1), 1, 1, past_len=18 + i)
+    dt = time.perf_counter() - t0
+    st.close()
+    return {"value": steps / dt, "unit": "tokens/s", "cores": num_threads(), "kind": "port",
+            "sample": f"{model.name} fp32 oracle (oracle/bloom_oracle.c), 1 stage, batch 1, KV-cached decode of "
+                      f"{steps} tokens after a 16-token prompt (+2 warm-up), {num_threads()} OpenMP threads; "
+                      f"weight generation {t_init:.1f}s excluded",
+            "cpu_model": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def bench_single(args):
+    import numpy as np
+    import torch
+    from distributed_inference_demo_amd import config
+    from distributed_inference_demo_amd.stage import Stage
+
+    m = config.get(args.model)
+    B, P, K, W = args.batch, args.prompt, args.steps, args.warmup
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    max_ctx = P + W + K + 1
+    st = Stage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, m.n_layer, dtype=args.dtype, device=0, max_batch=B,
+               max_ctx=max_ctx, max_tokens=max(B * P, B), seed=args.seed)
+    stream = torch.cuda.current_stream().cuda_stream
+    ids = torch.from_numpy(_prompt(B, P, m.vocab)).to(dev)
+    tok = torch.empty(B, dtype=torch.int32, device=dev)
+
+    # prefill (timed separately, bracketed by syncs)
+    torch.cuda.synchronize()
+    st.profile_enable(0 if args.no_profile else 2)
+    t0 = time.perf_counter()
+    st.forward(ids, tok, B, P, slot=0, past_len=0, stream=stream)
+    torch.cuda.synchronize()
+    t_prefill = time.perf_counter() - t0
+    pf_ms, pf_n, pf_flops = st.profile_read()
+    past = P
+    for _ in range(W):
+        st.forward(tok, tok, B, 1, slot=0, past_len=past, stream=stream)
+        past += 1
+    torch.cuda.synchronize()
+    st.profile_enable(0 if args.no_profile else 1)
+    t0 = time.perf_counter()
+    for _ in range(K):
+        st.forward(tok, tok, B, 1, slot=0, past_len=past, stream=stream)
+        past += 1
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    g_ms, g_n, g_bytes = st.profile_read()
+    ms_step = dt * 1e3 / K
+    ctx_mid = P + W + K / 2
+    step_bytes = config.decode_step_bytes(m, m.n_layer, B, ctx_mid, True, True,
+                                          w_bytes=2 if args.dtype == "bf16" else 4,
+                                          kv_bytes=2 if args.dtype == "bf16" else 4)
+    res = {
+        "metric": "decode tokens/s, BLOOM pipeline",
+        "value": B * K / dt, "unit": "tokens/s", "n_gpus": 1, "steps": K, "warmup": W,
+        "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic: repo-generator random-init weights (seed %d), prompt ids U[0,V) seed 1234" % args.seed,
+        "config": {"workload": f"{m.name} single stage on 1 MI355X, batch {B} decode after a {P}-token prefill "
+                               "(BASELINE.json configs[1])",
+                   "model": m.name, "stages": 1, "layers_per_stage": [m.n_layer], "batch": B, "prompt": P,
+                   "ctx_range": [P + W, P + W + K], "parallelism": "pp1"},
+    }
+    if not args.no_profile and g_n:
+        avg_ms = g_ms / g_n
+        ach = (g_bytes / g_n) / (avg_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "gemv_mfma_kernel (all decode weight GEMVs)",
+                           "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
+                           "traffic": None, "launches": g_n, "avg_us": avg_ms * 1e3,
+                           "algo_bytes_per_launch": g_bytes / g_n}
+    res["stage_hbm"] = {"algo_bytes_per_step": step_bytes, "achieved_GBps": step_bytes / (ms_step * 1e-3) / 1e9,
+                        "frac_of_peak": step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+    res["prefill"] = {"tokens": B * P, "ms": t_prefill * 1e3, "tokens_per_s": B * P / t_prefill,
+                      "algo_flops": config.prefill_flops(m, m.n_layer, B, P, True)}
+    res["prefill"]["achieved_TFLOPs"] = res["prefill"]["algo_flops"] / t_prefill / 1e12
+    if not args.no_profile and pf_n:
+        res["prefill"]["gemm_TFLOPs"] = pf_flops / (pf_ms * 1e-3) / 1e12
+        res["prefill"]["gemm_frac_of_peak"] = res["prefill"]["gemm_TFLOPs"] / BF16_PEAK_TFLOPS
+    st.close()
+    if args.cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(m, args.cpu_steps, args.seed)
+    return res
+
+
+def _prompt(B, P, V):
+    from distributed_inference_demo_amd.stage import prompt_ids
+    return prompt_ids(1234, B, P, V)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or args.gpus > 1:
+        from distributed_inference_demo_amd.pipeline import bench_pipeline
+        res = bench_pipeline(args)
+    else:
+        res = bench_single(args)
+    if res is not None:
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,63 @@
+"""Build libbloomstage.so (gfx950) in-tree with hipcc; no torch extension machinery.
+
+    python -m distributed_inference_demo_amd.build          # incremental
+    python -m distributed_inference_demo_amd.build --force
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OBJ = os.path.join(PKG, "build")
+LIB = os.path.join(PKG, "lib", "libbloomstage.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+SOURCES = ["kernels.hip", "stage.hip", "codec.cpp"]
+HEADERS = ["common.h", "kernels.h"]
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+          "-Wno-unused-variable", "-Wno-unused-result", "-Wno-unused-value", f"-I{os.path.join(ROOT, 'include')}"]
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else 0.0
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    hdr_t = max([_mtime(os.path.join(CSRC, h)) for h in HEADERS] + [_mtime(os.path.join(ROOT, "include", "bloomstage.h"))])
+    jobs = []
+    objs = []
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        op = os.path.join(OBJ, src + ".o")
+        objs.append(op)
+        if force or _mtime(op) < max(_mtime(sp), hdr_t):
+            flags = list(CFLAGS)
+            if src.endswith(".cpp"):
+                flags = [f for f in flags if not f.startswith("--offload-arch")] + ["-x", "c++"]
+            jobs.append([HIPCC] + flags + ["-c", sp, "-o", op])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return r.stderr
+
+    with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
+        for err in ex.map(run, jobs):
+            if err and verbose:
+                print(err)
+    if jobs or not os.path.exists(LIB) or any(_mtime(o) > _mtime(LIB) for o in objs):
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,71 @@
+// kernels.h — host-side launch wrappers for the stage kernels (implemented in kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// Epilogue of every weight GEMM/GEMV: y[m][n] = sum_k X[m][k] * W[n][k] (+ what `kind` says).
+enum EpiKind : int {
+  EPI_QKV = 0,     // + bias; q -> q_out fp32 [M][h]; k,v -> KV cache (T) at (slot+b, past+t)
+  EPI_RESID = 1,   // out_f32[m][n] = (y + bias) + resid[m][n]
+  EPI_GELU = 2,    // out_act[m][n] = T(gelu(y + bias))
+  EPI_ARGMAX = 3,  // no bias; 64-bit atomicMax of (order(y), ~n) into keys[m]; optional logits
+};
+
+struct Epi {
+  int kind;
+  const void* bias;       // T [N]
+  float* out_f32;         // EPI_RESID output [M][ldo]
+  void* out_act;          // EPI_GELU output (T) [M][ldo]
+  const float* resid;     // EPI_RESID residual [M][ldo]
+  int ldo;                // leading dim of out/resid (= N)
+  // EPI_QKV
+  float* q_out;           // [M][hidden]
+  void* k_cache;          // T, layer base of K: [max_batch][heads][max_ctx][hd]
+  void* v_cache;
+  int hidden, head_dim, max_ctx, n_head;
+  int seq, slot;
+  const int* past_dev;    // device scalar past_len (graph-replayable); used when non-null
+  int past;               // host past_len otherwise
+  // EPI_ARGMAX
+  unsigned long long* keys;  // [M][N/16]: max over each 16-column tile
+  float* logits;          // optional [M][ldo]
+};
+
+// dtype tag: 0 = fp32, 1 = bf16
+void launch_gen_fill(void* dst, int is_bf16, uint64_t n, uint64_t key, int kind, hipStream_t s);
+void launch_convert_f32(void* dst, int is_bf16, const float* src, uint64_t n, hipStream_t s);
+
+// LayerNorm rows: out[m] (T, or fp32 when out_f32) = LN(x[m*row_stride + row_offset]) with
+// gamma/beta (T); x is fp32 [.][K].  If ids != null, row m is instead gathered from the
+// embedding table `x` (T) [vocab][K] at ids[m] (word_embeddings + word_embeddings_layernorm).
+void launch_layernorm(int is_bf16, const void* x, const int* ids, int row_stride, int row_offset,
+                      const void* gamma, const void* beta, void* out, int out_f32, int M, int K,
+                      float eps, hipStream_t s);
+
+// Weight GEMM: X (T) [M][K] x W (T) [N][K]^T with epilogue.
+void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int K, const Epi& ep,
+                   hipStream_t s);
+
+// Attention over the KV cache for B rows x S new queries per row (causal, ALiBi).
+struct AttnArgs {
+  const float* q;      // [B*S][hidden] fp32
+  const void* k_cache; // T layer base
+  const void* v_cache;
+  void* ctx_out;       // T [B*S][hidden]
+  const float* slopes; // [n_head]
+  int B, S, slot;
+  const int* past_dev; // device past_len (graph-replayable) or null
+  int past;
+  int n_head, head_dim, max_ctx, hidden;
+  float inv_norm;
+  float* part_acc;     // workspace [B][n_head][max_chunks][head_dim]
+  float* part_ml;      // workspace [B][n_head][max_chunks][2]
+  int max_chunks;
+  int chunk;           // positions per split-K chunk (decode)
+};
+void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s);
+size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, int* max_chunks, int* chunk);
+
+// keys -> token ids
+void launch_argmax_finalize(const unsigned long long* keys, int* tokens, int M, int ntiles, hipStream_t s);
+void launch_set_past(int* past_dev, int value, hipStream_t s);

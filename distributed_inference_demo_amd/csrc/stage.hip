@@ -1,0 +1,562 @@
+// stage.hip — libbloomstage C-ABI (include/bloomstage.h): stage lifetime + forward orchestration.
+//
+// Replaces the reference's per-device stage execution:
+//   SessionCache / createSession (session_cache.h:20-35, native-lib.cpp:663-678)  -> bs_init_stage
+//   run_inference + JNI wrappers (inference.cpp:145-218, native-lib.cpp:942-1443)  -> bs_forward
+//   releaseSession (native-lib.cpp:1290-1303)                                       -> bs_release
+// Everything the ONNX sub-model computed on the CPU is here a sequence of gfx950 kernels
+// (kernels.hip) over weights, KV cache and workspace resident in the stage GPU's HBM.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/bloomstage.h"
+#include "kernels.h"
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(BS_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));        \
+  } while (0)
+
+namespace {
+
+enum { T_LN1_G, T_LN1_B, T_QKV_W, T_QKV_B, T_DENSE_W, T_DENSE_B, T_LN2_G, T_LN2_B, T_FC1_W, T_FC1_B,
+       T_FC2_W, T_FC2_B, T_NLAYER };
+enum { M_WEMB = 0, M_EMB_G = 1, M_EMB_B = 2, M_LNF_G = 3, M_LNF_B = 4 };
+
+struct Layer {
+  void* t[T_NLAYER];
+};
+
+struct ProfClass {
+  int cls = 0;
+  std::vector<hipEvent_t> ev;  // pairs
+  size_t used = 0;
+  double algo = 0.0;
+};
+
+}  // namespace
+
+struct bs_stage {
+  bs_stage_desc d;
+  int bf16 = 1;
+  size_t esz = 2;
+  int hd = 0, L = 0;
+  hipStream_t own = nullptr;
+  // HBM
+  char* wbase = nullptr;
+  size_t wbytes = 0;
+  void* wemb = nullptr;
+  void* emb_g = nullptr;
+  void* emb_b = nullptr;
+  void* lnf_g = nullptr;
+  void* lnf_b = nullptr;
+  std::vector<Layer> layers;
+  char* kv = nullptr;  // [L][2][max_batch][heads][max_ctx][hd]
+  size_t kvbytes = 0;
+  size_t kv_layer_stride = 0;  // bytes per (layer) = 2 * half
+  size_t kv_half = 0;          // bytes for K (or V) of one layer
+  char* ws = nullptr;
+  size_t wsbytes = 0;
+  float* xa = nullptr;   // fp32 [T][h]
+  float* xb = nullptr;   // fp32 [T][h]
+  float* attn = nullptr; // fp32 [T][h]
+  float* q = nullptr;    // fp32 [T][h]
+  void* xn = nullptr;    // act [T][h]
+  void* ctx = nullptr;   // act [T][h]
+  void* g = nullptr;     // act [T][4h]
+  float* part_acc = nullptr;
+  float* part_ml = nullptr;
+  int max_chunks = 0, chunk = 64;
+  float* slopes = nullptr;
+  unsigned long long* keys = nullptr;  // [max_batch][V/16]
+  int* tok = nullptr;                  // [max_batch]
+  int* ids = nullptr;                  // [T] staging for host ids
+  int* past_dev = nullptr;
+  ProfClass prof;
+  std::vector<std::pair<void*, size_t>> order;  // canonical weight order (BS_WEIGHTS_HOST layout)
+};
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static uint64_t host_sm64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+static uint64_t tensor_key(uint64_t seed, int layer, uint32_t tid) {
+  return host_sm64(seed ^ host_sm64(((uint64_t)(uint32_t)(layer + 1) << 8) | tid));
+}
+static int layer_kind(int tid) {
+  switch (tid) {
+    case T_LN1_G: case T_LN2_G: return 2;
+    case T_LN1_B: case T_LN2_B: return 3;
+    case T_QKV_W: case T_DENSE_W: case T_FC1_W: case T_FC2_W: return 0;
+    default: return 1;
+  }
+}
+static void layer_sizes(size_t h, size_t* sz) {
+  const size_t s[T_NLAYER] = {h, h, 3 * h * h, 3 * h, h * h, h, h, h, 4 * h * h, 4 * h, 4 * h * h, h};
+  for (int i = 0; i < T_NLAYER; i++) sz[i] = s[i];
+}
+
+// ALiBi slopes, build_alibi_tensor (modeling_bloom.py:60-78).
+static void alibi_slopes(int n_head, float* out) {
+  int cp2 = 1;
+  while (cp2 * 2 <= n_head) cp2 *= 2;
+  const float basef = (float)std::pow(2.0, -std::pow(2.0, -(std::log2((double)cp2) - 3.0)));
+  for (int i = 0; i < cp2; i++) out[i] = (float)std::pow((double)basef, (double)(i + 1));
+  if (cp2 != n_head) {
+    const float ebf = (float)std::pow(2.0, -std::pow(2.0, -(std::log2((double)(2 * cp2)) - 3.0)));
+    const int rem = std::min(n_head - cp2, cp2);
+    for (int i = 0; i < rem; i++) out[cp2 + i] = (float)std::pow((double)ebf, (double)(2 * i + 1));
+  }
+}
+
+static int validate(const bs_stage_desc* d) {
+  if (!d) return fail(BS_ERR_INVALID, "desc is NULL");
+  if (d->hidden <= 0 || d->n_head <= 0 || d->hidden % d->n_head)
+    return fail(BS_ERR_INVALID, "hidden must be a positive multiple of n_head");
+  if (d->hidden % 32) return fail(BS_ERR_INVALID, "hidden must be a multiple of 32");
+  const int hd = d->hidden / d->n_head;
+  if (hd % 8 || hd > 128) return fail(BS_ERR_INVALID, "head_dim must be a multiple of 8 and <= 128");
+  if (d->n_layer <= 0 || d->layer_begin < 0 || d->layer_end > d->n_layer || d->layer_begin > d->layer_end)
+    return fail(BS_ERR_INVALID, "bad layer range");
+  if (d->vocab <= 0 || d->vocab % 16) return fail(BS_ERR_INVALID, "vocab must be a positive multiple of 16");
+  if (d->dtype != BS_DT_BFLOAT16 && d->dtype != BS_DT_FLOAT) return fail(BS_ERR_INVALID, "dtype must be BFLOAT16 or FLOAT");
+  if (d->max_batch <= 0 || d->max_ctx <= 0) return fail(BS_ERR_INVALID, "max_batch/max_ctx must be positive");
+  if (!(d->ln_eps > 0.f)) return fail(BS_ERR_INVALID, "ln_eps must be positive");
+  if (d->weight_source != BS_WEIGHTS_SYNTHETIC && d->weight_source != BS_WEIGHTS_HOST)
+    return fail(BS_ERR_INVALID, "unknown weight_source");
+  return BS_OK;
+}
+
+extern "C" uint64_t bs_stage_weight_count(const bs_stage_desc* d) {
+  if (validate(d) != BS_OK) return 0;
+  const uint64_t h = (uint64_t)d->hidden;
+  uint64_t n = 0;
+  if (d->is_first || d->is_last) n += (uint64_t)d->vocab * h;
+  if (d->is_first) n += 2 * h;
+  n += (uint64_t)(d->layer_end - d->layer_begin) * (12 * h * h + 13 * h);
+  if (d->is_last) n += 2 * h;
+  return n;
+}
+
+extern "C" int bs_abi_version(void) { return BS_ABI_VERSION; }
+
+static uint32_t host_lb32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+
+extern "C" int bs_prompt_ids(uint64_t seed, int32_t n, int32_t vocab, int32_t* out) {
+  if (n < 0 || vocab <= 0 || (n && !out)) return fail(BS_ERR_INVALID, "bad prompt_ids arguments");
+  const uint64_t key = tensor_key(seed, -1, 255);
+  for (int32_t i = 0; i < n; i++)
+    out[i] = (int32_t)(host_lb32((uint32_t)key ^ host_lb32((uint32_t)i + (uint32_t)(key >> 32))) % (uint32_t)vocab);
+  return BS_OK;
+}
+extern "C" const char* bs_last_error(void) { return g_err.c_str(); }
+
+static void free_stage(bs_stage* s) {
+  if (!s) return;
+  hipSetDevice(s->d.device);
+  if (s->own) hipStreamSynchronize(s->own);
+  for (auto e : s->prof.ev) hipEventDestroy(e);
+  if (s->wbase) hipFree(s->wbase);
+  if (s->kv) hipFree(s->kv);
+  if (s->ws) hipFree(s->ws);
+  if (s->own) hipStreamDestroy(s->own);
+  delete s;
+}
+
+extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
+  if (!out) return fail(BS_ERR_INVALID, "out is NULL");
+  *out = nullptr;
+  int rc = validate(desc);
+  if (rc) return rc;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (desc->device < 0 || desc->device >= ndev) return fail(BS_ERR_INVALID, "device ordinal out of range");
+  HIP_TRY(hipSetDevice(desc->device));
+
+  bs_stage* s = new bs_stage();
+  s->d = *desc;
+  if (s->d.max_tokens <= 0) s->d.max_tokens = s->d.max_batch * 128;
+  s->bf16 = desc->dtype == BS_DT_BFLOAT16;
+  s->esz = s->bf16 ? 2 : 4;
+  s->hd = desc->hidden / desc->n_head;
+  s->L = desc->layer_end - desc->layer_begin;
+  const size_t h = desc->hidden, V = desc->vocab, T = s->d.max_tokens;
+
+  auto cleanup = [&](int code) { free_stage(s); return code; };
+  if (hipStreamCreateWithFlags(&s->own, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(BS_ERR_DEVICE, "hipStreamCreate failed"));
+
+  // ---- weight arena: every tensor 256-B aligned
+  std::vector<std::pair<void**, size_t>> plan;  // (slot, elements)
+  size_t off = 0;
+  std::vector<size_t> offs;
+  auto add = [&](size_t n) { offs.push_back(off); off = align_up(off + n * s->esz, 256); };
+  if (desc->is_first || desc->is_last) add(V * h);
+  if (desc->is_first) { add(h); add(h); }
+  size_t lsz[T_NLAYER];
+  layer_sizes(h, lsz);
+  for (int l = 0; l < s->L; l++)
+    for (int t = 0; t < T_NLAYER; t++) add(lsz[t]);
+  if (desc->is_last) { add(h); add(h); }
+  s->wbytes = off;
+  if (hipMalloc(&s->wbase, s->wbytes ? s->wbytes : 256) != hipSuccess)
+    return cleanup(fail(BS_ERR_OOM, "weight allocation failed (" + std::to_string(s->wbytes) + " B)"));
+  size_t oi = 0;
+  if (desc->is_first || desc->is_last) s->wemb = s->wbase + offs[oi++];
+  if (desc->is_first) { s->emb_g = s->wbase + offs[oi++]; s->emb_b = s->wbase + offs[oi++]; }
+  s->layers.resize(s->L);
+  for (int l = 0; l < s->L; l++)
+    for (int t = 0; t < T_NLAYER; t++) s->layers[l].t[t] = s->wbase + offs[oi++];
+  if (desc->is_last) { s->lnf_g = s->wbase + offs[oi++]; s->lnf_b = s->wbase + offs[oi++]; }
+  if (s->wemb) s->order.push_back({s->wemb, V * h});
+  if (s->emb_g) { s->order.push_back({s->emb_g, h}); s->order.push_back({s->emb_b, h}); }
+  for (int l = 0; l < s->L; l++)
+    for (int t = 0; t < T_NLAYER; t++) s->order.push_back({s->layers[l].t[t], lsz[t]});
+  if (s->lnf_g) { s->order.push_back({s->lnf_g, h}); s->order.push_back({s->lnf_b, h}); }
+
+  // ---- weights
+  if (desc->weight_source == BS_WEIGHTS_SYNTHETIC) {
+    const uint64_t seed = desc->seed;
+    if (s->wemb) launch_gen_fill(s->wemb, s->bf16, V * h, tensor_key(seed, -1, M_WEMB), 0, s->own);
+    if (s->emb_g) launch_gen_fill(s->emb_g, s->bf16, h, tensor_key(seed, -1, M_EMB_G), 2, s->own);
+    if (s->emb_b) launch_gen_fill(s->emb_b, s->bf16, h, tensor_key(seed, -1, M_EMB_B), 3, s->own);
+    for (int l = 0; l < s->L; l++)
+      for (int t = 0; t < T_NLAYER; t++)
+        launch_gen_fill(s->layers[l].t[t], s->bf16, lsz[t], tensor_key(seed, desc->layer_begin + l, t), layer_kind(t),
+                        s->own);
+    if (s->lnf_g) launch_gen_fill(s->lnf_g, s->bf16, h, tensor_key(seed, -1, M_LNF_G), 2, s->own);
+    if (s->lnf_b) launch_gen_fill(s->lnf_b, s->bf16, h, tensor_key(seed, -1, M_LNF_B), 3, s->own);
+  } else {
+    const uint64_t need = bs_stage_weight_count(desc);
+    if (!desc->host_weights || desc->host_weight_count != need)
+      return cleanup(fail(BS_ERR_INVALID, "host_weights count mismatch: need " + std::to_string(need)));
+    // canonical order == arena order; upload through an fp32 bounce buffer
+    const size_t chunk = 16u << 20;
+    float* bounce = nullptr;
+    if (hipMalloc(&bounce, chunk * sizeof(float)) != hipSuccess) return cleanup(fail(BS_ERR_OOM, "bounce alloc"));
+    const float* src = desc->host_weights;
+    for (auto& o : s->order) {
+      for (size_t i = 0; i < o.second; i += chunk) {
+        const size_t n = std::min(chunk, o.second - i);
+        if (hipMemcpyAsync(bounce, src + i, n * sizeof(float), hipMemcpyHostToDevice, s->own) != hipSuccess) {
+          hipFree(bounce);
+          return cleanup(fail(BS_ERR_DEVICE, "weight upload failed"));
+        }
+        launch_convert_f32((char*)o.first + i * s->esz, s->bf16, bounce, n, s->own);
+      }
+      src += o.second;
+    }
+    hipStreamSynchronize(s->own);
+    hipFree(bounce);
+  }
+
+  // ---- KV cache
+  s->kv_half = (size_t)desc->max_batch * desc->n_head * desc->max_ctx * s->hd * s->esz;
+  s->kv_layer_stride = 2 * s->kv_half;
+  s->kvbytes = s->kv_layer_stride * (s->L > 0 ? s->L : 0);
+  if (s->kvbytes) {
+    if (hipMalloc(&s->kv, s->kvbytes) != hipSuccess)
+      return cleanup(fail(BS_ERR_OOM, "KV cache allocation failed (" + std::to_string(s->kvbytes) + " B)"));
+    if (hipMemsetAsync(s->kv, 0, s->kvbytes, s->own) != hipSuccess) return cleanup(fail(BS_ERR_DEVICE, "kv memset"));
+  }
+
+  // ---- workspace
+  const size_t attn_f = attention_workspace_floats(desc->max_batch, desc->n_head, s->hd, desc->max_ctx, &s->max_chunks,
+                                                   &s->chunk);
+  std::vector<size_t> wo;
+  size_t woff = 0;
+  auto wadd = [&](size_t bytes) { wo.push_back(woff); woff = align_up(woff + bytes, 256); };
+  wadd(T * h * 4);       // xa
+  wadd(T * h * 4);       // xb
+  wadd(T * h * 4);       // attn
+  wadd(T * h * 4);       // q
+  wadd(T * h * s->esz);  // xn
+  wadd(T * h * s->esz);  // ctx
+  wadd(T * 4 * h * s->esz);  // g
+  wadd(attn_f * 4);      // partials
+  wadd(desc->n_head * 4);
+  wadd((size_t)desc->max_batch * (V / 16) * 8);
+  wadd((size_t)desc->max_batch * 4);
+  wadd(T * 4);
+  wadd(256);
+  s->wsbytes = woff;
+  if (hipMalloc(&s->ws, s->wsbytes) != hipSuccess) return cleanup(fail(BS_ERR_OOM, "workspace allocation failed"));
+  int wi = 0;
+  s->xa = (float*)(s->ws + wo[wi++]);
+  s->xb = (float*)(s->ws + wo[wi++]);
+  s->attn = (float*)(s->ws + wo[wi++]);
+  s->q = (float*)(s->ws + wo[wi++]);
+  s->xn = s->ws + wo[wi++];
+  s->ctx = s->ws + wo[wi++];
+  s->g = s->ws + wo[wi++];
+  s->part_acc = (float*)(s->ws + wo[wi++]);
+  s->part_ml = s->part_acc + (size_t)desc->max_batch * desc->n_head * s->max_chunks * s->hd;
+  s->slopes = (float*)(s->ws + wo[wi++]);
+  s->keys = (unsigned long long*)(s->ws + wo[wi++]);
+  s->tok = (int*)(s->ws + wo[wi++]);
+  s->ids = (int*)(s->ws + wo[wi++]);
+  s->past_dev = (int*)(s->ws + wo[wi++]);
+  std::vector<float> sl(desc->n_head);
+  alibi_slopes(desc->n_head, sl.data());
+  HIP_TRY(hipMemcpyAsync(s->slopes, sl.data(), sl.size() * 4, hipMemcpyHostToDevice, s->own));
+  hipError_t e = hipStreamSynchronize(s->own);
+  if (e != hipSuccess) return cleanup(fail(BS_ERR_DEVICE, std::string("init sync: ") + hipGetErrorString(e)));
+  e = hipGetLastError();
+  if (e != hipSuccess) return cleanup(fail(BS_ERR_DEVICE, std::string("init kernels: ") + hipGetErrorString(e)));
+  *out = s;
+  return BS_OK;
+}
+
+extern "C" void bs_release(bs_stage* s) { free_stage(s); }
+
+extern "C" int bs_stage_info(const bs_stage* s, bs_stage_desc* d, uint64_t* wb, uint64_t* kvb, uint64_t* wsb) {
+  if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
+  if (d) *d = s->d;
+  if (wb) *wb = s->wbytes;
+  if (kvb) *kvb = s->kvbytes;
+  if (wsb) *wsb = s->wsbytes;
+  return BS_OK;
+}
+
+extern "C" int bs_read_weights(const bs_stage* s, uint64_t offset, uint64_t count, float* out) {
+  if (!s || (count && !out)) return fail(BS_ERR_INVALID, "stage/out is NULL");
+  HIP_TRY(hipSetDevice(s->d.device));
+  HIP_TRY(hipStreamSynchronize(s->own));
+  uint64_t base = 0, done = 0;
+  std::vector<uint16_t> tmp;
+  for (const auto& o : s->order) {
+    const uint64_t b = base, e = base + o.second;
+    base = e;
+    if (e <= offset || b >= offset + count) continue;
+    const uint64_t lo = std::max<uint64_t>(b, offset), hi = std::min<uint64_t>(e, offset + count);
+    const uint64_t n = hi - lo;
+    const char* src = (const char*)o.first + (lo - b) * s->esz;
+    float* dst = out + (lo - offset);
+    if (s->bf16) {
+      tmp.resize(n);
+      HIP_TRY(hipMemcpy(tmp.data(), src, n * 2, hipMemcpyDeviceToHost));
+      for (uint64_t i = 0; i < n; i++) {
+        uint32_t u = (uint32_t)tmp[i] << 16;
+        std::memcpy(&dst[i], &u, 4);
+      }
+    } else {
+      HIP_TRY(hipMemcpy(dst, src, n * 4, hipMemcpyDeviceToHost));
+    }
+    done += n;
+  }
+  if (done != count) return fail(BS_ERR_INVALID, "read range outside the stage weights");
+  return BS_OK;
+}
+
+extern "C" int bs_reset_kv(bs_stage* s, int32_t slot) {
+  if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
+  if (slot >= s->d.max_batch) return fail(BS_ERR_INVALID, "slot out of range");
+  HIP_TRY(hipSetDevice(s->d.device));
+  // Cached positions are addressed by past_len, so forgetting is bookkeeping only; zero the
+  // rows anyway so stale data can never be read by a caller that reuses past_len wrongly.
+  const size_t row = (size_t)s->d.n_head * s->d.max_ctx * s->hd * s->esz;
+  for (int l = 0; l < s->L; l++)
+    for (int w = 0; w < 2; w++) {
+      char* base = s->kv + l * s->kv_layer_stride + w * s->kv_half;
+      if (slot < 0) HIP_TRY(hipMemsetAsync(base, 0, s->kv_half, s->own));
+      else HIP_TRY(hipMemsetAsync(base + (size_t)slot * row, 0, row, s->own));
+    }
+  HIP_TRY(hipStreamSynchronize(s->own));
+  return BS_OK;
+}
+
+// ---- profiling
+extern "C" int bs_profile_enable(bs_stage* s, int32_t cls) {
+  if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
+  s->prof.cls = cls;
+  s->prof.used = 0;
+  s->prof.algo = 0.0;
+  return BS_OK;
+}
+
+static hipEvent_t prof_event(bs_stage* s) {
+  if (s->prof.used >= s->prof.ev.size()) {
+    hipEvent_t e;
+    hipEventCreate(&e);
+    s->prof.ev.push_back(e);
+  }
+  return s->prof.ev[s->prof.used++];
+}
+
+extern "C" int bs_profile_read(bs_stage* s, double* total_ms, uint64_t* launches, double* algo) {
+  if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
+  double tot = 0.0;
+  for (size_t i = 0; i + 1 < s->prof.used; i += 2) {
+    HIP_TRY(hipEventSynchronize(s->prof.ev[i + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, s->prof.ev[i], s->prof.ev[i + 1]));
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = s->prof.used / 2;
+  if (algo) *algo = s->prof.algo;
+  return BS_OK;
+}
+
+namespace {
+struct ProfScope {
+  bs_stage* s;
+  hipStream_t st;
+  bool on;
+  ProfScope(bs_stage* s_, hipStream_t st_, int cls, double units) : s(s_), st(st_), on(s_->prof.cls == cls && cls) {
+    if (on) {
+      hipEventRecord(prof_event(s), st);
+      s->prof.algo += units;
+    }
+  }
+  ~ProfScope() {
+    if (on) hipEventRecord(prof_event(s), st);
+  }
+};
+}  // namespace
+
+// Algorithmic bytes of one weight GEMV launch (decode): weights + bias + activations in/out.
+static double gemv_bytes(const bs_stage* s, int M, int N, int K, int out_bytes) {
+  return (double)N * K * s->esz + (double)N * s->esz + (double)M * K * s->esz + (double)M * N * out_bytes;
+}
+
+static void linear(bs_stage* s, hipStream_t st, const void* X, const void* W, int M, int N, int K, const Epi& ep,
+                   int out_bytes) {
+  const bool decode = M <= 32 && s->bf16;
+  if (decode) {
+    ProfScope p(s, st, 1, gemv_bytes(s, M, N, K, out_bytes));
+    launch_linear(s->bf16, X, W, M, N, K, ep, st);
+  } else {
+    ProfScope p(s, st, 2, 2.0 * M * N * K);
+    launch_linear(s->bf16, X, W, M, N, K, ep, st);
+  }
+}
+
+extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void* out, float* logits, void* stream) {
+  if (!s || !step) return fail(BS_ERR_INVALID, "stage/step is NULL");
+  const bs_stage_desc& d = s->d;
+  const int B = step->batch, S = step->seq, slot = step->slot, past = step->past_len;
+  const int M = B * S;
+  if (B <= 0 || S <= 0) return fail(BS_ERR_INVALID, "batch and seq must be positive");
+  if (slot < 0 || slot + B > d.max_batch) return fail(BS_ERR_INVALID, "slot range outside max_batch");
+  if (past < 0 || past + S > d.max_ctx) return fail(BS_ERR_INVALID, "past_len + seq exceeds max_ctx");
+  if (M > d.max_tokens) return fail(BS_ERR_INVALID, "batch*seq exceeds max_tokens");
+  if (!in || !out) return fail(BS_ERR_INVALID, "in/out is NULL");
+  const bool want_logits = (step->flags & BS_STEP_LOGITS) != 0;
+  if (want_logits && (!d.is_last || !logits)) return fail(BS_ERR_INVALID, "logits requested on a non-last stage or NULL");
+  const bool host_io = (step->flags & BS_STEP_HOST_IO) != 0;
+  HIP_TRY(hipSetDevice(d.device));
+  hipStream_t st = stream ? (hipStream_t)stream : s->own;
+  const int h = d.hidden, V = d.vocab, hd = s->hd, nh = d.n_head;
+
+  // ---- input
+  const float* cur = nullptr;
+  if (d.is_first) {
+    const int* ids = (const int*)in;
+    if (host_io) {
+      for (int i = 0; i < M; i++)
+        if (ids[i] < 0 || ids[i] >= V) return fail(BS_ERR_INVALID, "token id out of range");
+      HIP_TRY(hipMemcpyAsync(s->ids, ids, (size_t)M * 4, hipMemcpyHostToDevice, st));
+      ids = s->ids;
+    }
+    launch_layernorm(s->bf16, s->wemb, ids, 0, 0, s->emb_g, s->emb_b, s->xa, 1, M, h, d.ln_eps, st);
+    cur = s->xa;
+  } else if (host_io) {
+    HIP_TRY(hipMemcpyAsync(s->xa, in, (size_t)M * h * 4, hipMemcpyHostToDevice, st));
+    cur = s->xa;
+  } else {
+    cur = (const float*)in;
+  }
+
+  // ---- decoder blocks
+  const float inv_norm = 1.0f / std::sqrt((float)hd);
+  for (int l = 0; l < s->L; l++) {
+    const Layer& w = s->layers[l];
+    char* kbase = s->kv + l * s->kv_layer_stride;
+    // x1 = LN_in(x)
+    launch_layernorm(s->bf16, cur, nullptr, 1, 0, w.t[T_LN1_G], w.t[T_LN1_B], s->xn, 0, M, h, d.ln_eps, st);
+    // fused QKV (+bias) -> q, K/V cache
+    Epi e{};
+    e.kind = EPI_QKV; e.bias = w.t[T_QKV_B]; e.q_out = s->q; e.k_cache = kbase; e.v_cache = kbase + s->kv_half;
+    e.hidden = h; e.head_dim = hd; e.max_ctx = d.max_ctx; e.n_head = nh; e.seq = S; e.slot = slot; e.past = past;
+    e.ldo = 3 * h;
+    linear(s, st, s->xn, w.t[T_QKV_W], M, 3 * h, h, e, 4);
+    // attention
+    AttnArgs a{};
+    a.q = s->q; a.k_cache = kbase; a.v_cache = kbase + s->kv_half; a.ctx_out = s->ctx; a.slopes = s->slopes;
+    a.B = B; a.S = S; a.slot = slot; a.past = past; a.n_head = nh; a.head_dim = hd; a.max_ctx = d.max_ctx;
+    a.hidden = h; a.inv_norm = inv_norm; a.part_acc = s->part_acc; a.part_ml = s->part_ml;
+    a.max_chunks = s->max_chunks; a.chunk = s->chunk;
+    {
+      ProfScope p(s, st, 3, (double)B * nh * (double)(past + S) * hd * 2 * s->esz);
+      launch_attention(s->bf16, a, st);
+    }
+    // a = x + dense(ctx)
+    Epi e2{};
+    e2.kind = EPI_RESID; e2.bias = w.t[T_DENSE_B]; e2.out_f32 = s->attn; e2.resid = cur; e2.ldo = h;
+    linear(s, st, s->ctx, w.t[T_DENSE_W], M, h, h, e2, 4);
+    // x2 = LN_post(a); g = gelu(x2 W1 + b1)
+    launch_layernorm(s->bf16, s->attn, nullptr, 1, 0, w.t[T_LN2_G], w.t[T_LN2_B], s->xn, 0, M, h, d.ln_eps, st);
+    Epi e3{};
+    e3.kind = EPI_GELU; e3.bias = w.t[T_FC1_B]; e3.out_act = s->g; e3.ldo = 4 * h;
+    linear(s, st, s->xn, w.t[T_FC1_W], M, 4 * h, h, e3, (int)s->esz);
+    // x = a + g W2 + b2
+    float* nxt = (!d.is_last && !host_io && l == s->L - 1) ? (float*)out : (cur == s->xa ? s->xb : s->xa);
+    Epi e4{};
+    e4.kind = EPI_RESID; e4.bias = w.t[T_FC2_B]; e4.out_f32 = nxt; e4.resid = s->attn; e4.ldo = h;
+    linear(s, st, s->g, w.t[T_FC2_W], M, h, 4 * h, e4, 4);
+    cur = nxt;
+  }
+
+  // ---- output
+  if (d.is_last) {
+    // ln_f on each row's last position, tied lm_head, greedy pick
+    launch_layernorm(s->bf16, cur, nullptr, S, S - 1, s->lnf_g, s->lnf_b, s->xn, 0, B, h, d.ln_eps, st);
+    Epi e{};
+    e.kind = EPI_ARGMAX; e.keys = s->keys; e.logits = want_logits && !host_io ? logits : nullptr; e.ldo = V;
+    float* dev_logits = nullptr;
+    if (want_logits && host_io) {
+      // logits go through the attention-partials-free region of the workspace? keep it simple: temp alloc
+      HIP_TRY(hipMallocAsync((void**)&dev_logits, (size_t)B * V * 4, st));
+      e.logits = dev_logits;
+    }
+    linear(s, st, s->xn, s->wemb, B, V, h, e, 0);
+    launch_argmax_finalize(s->keys, host_io ? s->tok : (int*)out, B, V / 16, st);
+    if (host_io) {
+      HIP_TRY(hipMemcpyAsync(out, s->tok, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+      if (dev_logits) {
+        HIP_TRY(hipMemcpyAsync(logits, dev_logits, (size_t)B * V * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipFreeAsync(dev_logits, st));
+      }
+    }
+  } else if (host_io) {
+    HIP_TRY(hipMemcpyAsync(out, cur, (size_t)M * h * 4, hipMemcpyDeviceToHost, st));
+  } else if (s->L == 0) {
+    HIP_TRY(hipMemcpyAsync(out, cur, (size_t)M * h * 4, hipMemcpyDeviceToDevice, st));
+  }
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return fail(BS_ERR_DEVICE, std::string("kernel launch: ") + hipGetErrorString(err));
+  if (host_io) HIP_TRY(hipStreamSynchronize(st));
+  return BS_OK;
+}

@@ -1,0 +1,364 @@
+"""ctypes binding of libbloomstage.so + the host-side mirror of the reference's stage interface.
+
+Reference interface (Java side `Communication.java:1153-1182`, C++ side `native-lib.cpp`):
+
+    long   createSession(String modelPath)                                   native-lib.cpp:671-678
+    void   releaseSession(long session)                                      native-lib.cpp:1290-1303
+    Object[] runInferenceMasterResidual(long, int[] ids, int[] seq, int[][] res)   :942-1034
+    Object[] runInferenceWorkerResidual(long, byte[] seq, ArrayList<byte[]> res, int[], int[][])  :1036-1194
+    byte[] runInferenceWorkerResidualLastGeneration(long, byte[] seq, ArrayList<byte[]> res, int k, float temp)  :1368-1443
+    int    deserializeInt(byte[])                                            :1445-1471
+
+`create_session`, `release_session`, `run_inference_master_residual`,
+`run_inference_worker_residual`, `run_inference_worker_residual_last_generation` and
+`deserialize_int` below keep those names, argument meanings and wire formats (activations as
+the utils.cpp tensor-vector bytes, the tail's token as 4 little-endian bytes) so the
+reference's driver loop ports over unchanged.  They run the stage with host I/O.  The fast
+path is `Stage.forward()` on device buffers (what the RCCL pipeline uses).
+
+Behavioural differences, all deliberate (DESIGN.md "Boundary"): errors raise `BloomStageError`
+with the library's message instead of C++ exceptions crossing JNI; the header stage feeds the
+whole new-token slice and keeps a KV cache (the reference feeds only the last token with no
+cache, Communication.java:322-326, so it ignores context); the tail picks the greedy argmax
+(k == 1) or a seeded top-k sample (k > 1) rather than an unseeded one (decoding.cpp:61-63).
+"""
+import ctypes
+import os
+import struct
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "lib", "libbloomstage.so")
+
+BS_DT_FLOAT = 1
+BS_DT_BFLOAT16 = 16
+BS_WEIGHTS_SYNTHETIC = 0
+BS_WEIGHTS_HOST = 1
+BS_STEP_HOST_IO = 1
+BS_STEP_LOGITS = 2
+
+DTYPES = {
+    1: np.float32, 2: np.uint8, 3: np.int8, 4: np.uint16, 5: np.int16, 6: np.int32, 7: np.int64,
+    9: np.bool_, 11: np.float64, 12: np.uint32, 13: np.uint64,
+}
+NP_TO_DT = {np.dtype(v): k for k, v in DTYPES.items()}
+
+
+class BloomStageError(RuntimeError):
+    pass
+
+
+class StageDesc(ctypes.Structure):
+    _fields_ = [
+        ("hidden", ctypes.c_int32), ("n_head", ctypes.c_int32), ("n_layer", ctypes.c_int32),
+        ("vocab", ctypes.c_int32), ("ln_eps", ctypes.c_float),
+        ("layer_begin", ctypes.c_int32), ("layer_end", ctypes.c_int32),
+        ("is_first", ctypes.c_int32), ("is_last", ctypes.c_int32),
+        ("dtype", ctypes.c_int32), ("device", ctypes.c_int32),
+        ("max_batch", ctypes.c_int32), ("max_ctx", ctypes.c_int32), ("max_tokens", ctypes.c_int32),
+        ("weight_source", ctypes.c_int32), ("seed", ctypes.c_uint64),
+        ("host_weights", ctypes.c_void_p), ("host_weight_count", ctypes.c_uint64),
+        ("flags", ctypes.c_int32),
+    ]
+
+
+class Step(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("seq", ctypes.c_int32), ("slot", ctypes.c_int32),
+                ("past_len", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+class TensorView(ctypes.Structure):
+    _fields_ = [("dtype", ctypes.c_int32), ("ndim", ctypes.c_int32), ("dims", ctypes.c_int64 * 8),
+                ("data", ctypes.c_void_p)]
+
+
+EXPORTS = [
+    "bs_init_stage", "bs_forward", "bs_reset_kv", "bs_release", "bs_last_error", "bs_stage_info",
+    "bs_stage_weight_count", "bs_abi_version", "bs_profile_enable", "bs_profile_read",
+    "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
+    "bs_prompt_ids", "bs_read_weights",
+]
+
+_LIB = None
+
+
+def lib():
+    """Load the HIP library.  There is no CPU fallback: a missing library is an error."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise BloomStageError(f"{LIB_PATH} not built: run `python -m distributed_inference_demo_amd.build`")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32 = ctypes.c_void_p, ctypes.c_int32
+        L.bs_init_stage.argtypes = [ctypes.POINTER(StageDesc), ctypes.POINTER(vp)]
+        L.bs_forward.argtypes = [vp, ctypes.POINTER(Step), vp, vp, vp, vp]
+        L.bs_reset_kv.argtypes = [vp, i32]
+        L.bs_release.argtypes = [vp]
+        L.bs_release.restype = None
+        L.bs_last_error.restype = ctypes.c_char_p
+        L.bs_stage_info.argtypes = [vp, ctypes.POINTER(StageDesc)] + [ctypes.POINTER(ctypes.c_uint64)] * 3
+        L.bs_stage_weight_count.argtypes = [ctypes.POINTER(StageDesc)]
+        L.bs_stage_weight_count.restype = ctypes.c_uint64
+        L.bs_profile_enable.argtypes = [vp, i32]
+        L.bs_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_double)]
+        L.bs_codec_serialize.argtypes = [ctypes.POINTER(TensorView), i32, vp, ctypes.c_uint64]
+        L.bs_codec_serialize.restype = ctypes.c_int64
+        L.bs_codec_deserialize.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(TensorView), i32, ctypes.POINTER(i32)]
+        L.bs_dtype_size.argtypes = [i32]
+        L.bs_dtype_size.restype = ctypes.c_int64
+        L.bs_serialize_int.argtypes = [i32, ctypes.c_char_p]
+        L.bs_serialize_int.restype = None
+        L.bs_deserialize_int.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(i32)]
+        L.bs_prompt_ids.argtypes = [ctypes.c_uint64, i32, i32, vp]
+        L.bs_read_weights.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, vp]
+        _LIB = L
+    return _LIB
+
+
+def _check(rc):
+    if rc != 0:
+        raise BloomStageError(f"bloomstage error {rc}: {lib().bs_last_error().decode(errors='replace')}")
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    if hasattr(x, "data_ptr"):  # torch tensor
+        return x.data_ptr()
+    raise TypeError(f"cannot take a pointer of {type(x)}")
+
+
+class Stage:
+    """One pipeline stage (contiguous layer range) resident on one GPU."""
+
+    def __init__(self, hidden, n_head, n_layer, vocab, layer_begin, layer_end, *, dtype="bf16", device=0,
+                 max_batch=1, max_ctx=2048, max_tokens=0, seed=0, eps=1e-5, host_weights=None,
+                 is_first=None, is_last=None):
+        d = StageDesc()
+        d.hidden, d.n_head, d.n_layer, d.vocab, d.ln_eps = hidden, n_head, n_layer, vocab, eps
+        d.layer_begin, d.layer_end = layer_begin, layer_end
+        d.is_first = int(layer_begin == 0 if is_first is None else is_first)
+        d.is_last = int(layer_end == n_layer if is_last is None else is_last)
+        d.dtype = BS_DT_BFLOAT16 if dtype in ("bf16", BS_DT_BFLOAT16) else BS_DT_FLOAT
+        d.device, d.max_batch, d.max_ctx, d.max_tokens = device, max_batch, max_ctx, max_tokens
+        d.seed = seed
+        self._weights_ref = None
+        if host_weights is not None:
+            w = np.ascontiguousarray(host_weights, dtype=np.float32).reshape(-1)
+            self._weights_ref = w
+            d.weight_source = BS_WEIGHTS_HOST
+            d.host_weights = w.ctypes.data
+            d.host_weight_count = w.size
+        else:
+            d.weight_source = BS_WEIGHTS_SYNTHETIC
+        self.desc = d
+        self.hidden, self.vocab = hidden, vocab
+        self.is_first, self.is_last = bool(d.is_first), bool(d.is_last)
+        self.max_batch, self.max_ctx = max_batch, max_ctx
+        h = ctypes.c_void_p()
+        _check(lib().bs_init_stage(ctypes.byref(d), ctypes.byref(h)))
+        self._h = h
+        self._weights_ref = None  # uploaded; host copy no longer needed
+        self.past = [0] * max_batch  # host mirror of cached positions per KV row
+
+    # ---- fast path (device pointers, stream ordered)
+    def forward(self, inp, out, batch, seq, slot=0, past_len=None, logits=None, stream=None):
+        past = self.past[slot] if past_len is None else past_len
+        st = Step(batch, seq, slot, past, BS_STEP_LOGITS if logits is not None else 0)
+        _check(lib().bs_forward(self._h, ctypes.byref(st), _ptr(inp), _ptr(out), _ptr(logits), stream))
+        for r in range(slot, slot + batch):
+            self.past[r] = past + seq
+        return out
+
+    # ---- host I/O convenience (numpy in, numpy out)
+    def forward_host(self, x, batch, seq, slot=0, past_len=None, want_logits=False):
+        if self.is_first:
+            x = np.ascontiguousarray(x, dtype=np.int32).reshape(batch, seq)
+        else:
+            x = np.ascontiguousarray(x, dtype=np.float32).reshape(batch, seq, self.hidden)
+        out = np.empty(batch, np.int32) if self.is_last else np.empty((batch, seq, self.hidden), np.float32)
+        logits = np.empty((batch, self.vocab), np.float32) if want_logits else None
+        past = self.past[slot] if past_len is None else past_len
+        flags = BS_STEP_HOST_IO | (BS_STEP_LOGITS if want_logits else 0)
+        st = Step(batch, seq, slot, past, flags)
+        _check(lib().bs_forward(self._h, ctypes.byref(st), x.ctypes.data, out.ctypes.data,
+                                logits.ctypes.data if logits is not None else None, None))
+        for r in range(slot, slot + batch):
+            self.past[r] = past + seq
+        return (out, logits) if want_logits else out
+
+    def reset(self, slot=-1):
+        _check(lib().bs_reset_kv(self._h, slot))
+        if slot < 0:
+            self.past = [0] * self.max_batch
+        else:
+            self.past[slot] = 0
+
+    def info(self):
+        d = StageDesc()
+        wb, kb, sb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().bs_stage_info(self._h, ctypes.byref(d), ctypes.byref(wb), ctypes.byref(kb), ctypes.byref(sb)))
+        return {"weight_bytes": wb.value, "kv_bytes": kb.value, "workspace_bytes": sb.value}
+
+    def read_weights(self, offset=0, count=None):
+        """Weights in canonical stage order (BS_WEIGHTS_HOST layout) as fp32."""
+        if count is None:
+            count = lib().bs_stage_weight_count(ctypes.byref(self.desc)) - offset
+        out = np.empty(count, np.float32)
+        _check(lib().bs_read_weights(self._h, offset, count, out.ctypes.data))
+        return out
+
+    def profile_enable(self, kernel_class):
+        _check(lib().bs_profile_enable(self._h, kernel_class))
+
+    def profile_read(self):
+        ms, n, units = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_double()
+        _check(lib().bs_profile_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(units)))
+        return ms.value, n.value, units.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().bs_release(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def prompt_ids(seed, batch, seq, vocab):
+    """Synthetic prompt ids [batch][seq] (repo generator, computed by the library)."""
+    out = np.empty((batch, seq), np.int32)
+    _check(lib().bs_prompt_ids(seed, batch * seq, vocab, out.ctypes.data))
+    return out
+
+
+def weight_count(**kw):
+    d = StageDesc()
+    for k, v in kw.items():
+        setattr(d, k, v)
+    return lib().bs_stage_weight_count(ctypes.byref(d))
+
+
+# ---------------------------------------------------------------------------------------
+# Wire codec (utils.cpp:124-368) through the C library.
+# ---------------------------------------------------------------------------------------
+def serialize_tensors(arrays) -> bytes:
+    """SerializeTensorVectorToBytes (utils.cpp:124-264)."""
+    arrays = [np.asarray(a) for a in arrays]
+    arrays = [a if a.flags.c_contiguous else a.copy(order="C") for a in arrays]  # keeps 0-d shapes
+    views = (TensorView * max(1, len(arrays)))()
+    for i, a in enumerate(arrays):
+        if a.dtype not in NP_TO_DT:
+            raise BloomStageError(f"dtype {a.dtype} is not carried by the reference wire codec")
+        views[i].dtype = NP_TO_DT[a.dtype]
+        views[i].ndim = a.ndim
+        for k, s in enumerate(a.shape):
+            views[i].dims[k] = s
+        views[i].data = a.ctypes.data if a.size else None
+    n = lib().bs_codec_serialize(views, len(arrays), None, 0)
+    if n < 0:
+        raise BloomStageError(f"serialize failed ({n})")
+    buf = ctypes.create_string_buffer(n)
+    m = lib().bs_codec_serialize(views, len(arrays), buf, n)
+    if m != n:
+        raise BloomStageError(f"serialize failed ({m})")
+    return buf.raw
+
+
+def deserialize_tensors(data: bytes):
+    """DeserializeTensorVectorFromBytes (utils.cpp:266-368); returns copies as numpy arrays."""
+    n = ctypes.c_int32()
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    rc = lib().bs_codec_deserialize(buf, len(data), None, 0, ctypes.byref(n))
+    if rc != 0:
+        raise BloomStageError(f"deserialize failed ({rc})")
+    views = (TensorView * max(1, n.value))()
+    _check(lib().bs_codec_deserialize(buf, len(data), views, n.value, ctypes.byref(n)))
+    base = ctypes.addressof(buf)
+    out = []
+    for i in range(n.value):
+        v = views[i]
+        dt = np.dtype(DTYPES[v.dtype])
+        shape = tuple(v.dims[k] for k in range(v.ndim))
+        cnt = int(np.prod(shape)) if shape else 1
+        off = (v.data or base) - base
+        out.append(np.frombuffer(buf.raw, dtype=dt, count=cnt, offset=off).reshape(shape).copy())
+    return out
+
+
+def serialize_int(value: int) -> bytes:
+    """SerializeInt (utils.cpp:11-15): 4 native little-endian bytes."""
+    b = ctypes.create_string_buffer(4)
+    lib().bs_serialize_int(value, b)
+    return b.raw
+
+
+def deserialize_int(data: bytes) -> int:
+    """Java_..._deserializeInt (native-lib.cpp:1445-1471) / utils::DeserializeInt (utils.cpp:17-25)."""
+    v = ctypes.c_int32()
+    _check(lib().bs_deserialize_int(bytes(data), len(data), ctypes.byref(v)))
+    return v.value
+
+
+# ---------------------------------------------------------------------------------------
+# JNI-mirror entry points (host I/O, one sample per session like the reference).
+# ---------------------------------------------------------------------------------------
+def create_session(model, layer_begin, layer_end, **kw) -> Stage:
+    """createSession (native-lib.cpp:671-678): one module == one contiguous layer range of `model`
+    (a BloomDims from .config) on a GPU."""
+    return Stage(model.hidden, model.n_head, model.n_layer, model.vocab, layer_begin, layer_end, **kw)
+
+
+def release_session(stage: Stage) -> None:
+    """releaseSession (native-lib.cpp:1290-1303)."""
+    stage.close()
+
+
+def run_inference_master_residual(stage: Stage, input_ids, to_send_seq_indices=(0,), to_send_res_indices=()):
+    """runInferenceMasterResidual (native-lib.cpp:942-1034): header stage on new token ids.
+    Returns (seq_bytes, [residual_bytes...]) like the JNI Object[]{byte[], byte[][]}; this build
+    forwards only the hidden state, so the residual list is empty."""
+    if not stage.is_first:
+        raise BloomStageError("master (header) entry called on a non-first stage")
+    ids = np.asarray(input_ids, dtype=np.int32).reshape(1, -1)
+    hidden = stage.forward_host(ids, 1, ids.shape[1])
+    return serialize_tensors([hidden]), []
+
+
+def run_inference_worker_residual(stage: Stage, seq_bytes: bytes, residuals=(), to_send_seq_indices=(0,),
+                                  to_send_res_indices=()):
+    """runInferenceWorkerResidual (native-lib.cpp:1036-1194): middle stage, wire bytes in/out."""
+    tensors = deserialize_tensors(seq_bytes)
+    x = tensors[0].astype(np.float32, copy=False)
+    S = x.shape[-2]
+    hidden = stage.forward_host(x, 1, S)
+    return serialize_tensors([hidden]), []
+
+
+def run_inference_worker_residual_last_generation(stage: Stage, seq_bytes: bytes, residuals=(), k: int = 1,
+                                                  initial_temp: float = 1.0, seed: int = 0) -> bytes:
+    """runInferenceWorkerResidualLastGeneration (native-lib.cpp:1368-1443): tail stage, returns the
+    next token id as 4 little-endian bytes (utils::SerializeInt)."""
+    tensors = deserialize_tensors(seq_bytes)
+    x = tensors[0].astype(np.float32, copy=False)
+    S = x.shape[-2]
+    if k <= 1:
+        tok = stage.forward_host(x, 1, S)
+        return serialize_int(int(tok[0]))
+    tok, logits = stage.forward_host(x, 1, S, want_logits=True)
+    from .sampling import top_k_sample
+    return serialize_int(top_k_sample(logits[0], k, initial_temp, seed))
+
+
+def unpack_int_be(data: bytes) -> int:
+    """Java-side big-endian int codec (Utils.java:107-125), for the sample-id frames."""
+    return struct.unpack(">i", data)[0]

@@ -1,0 +1,162 @@
+/*
+ * bloomstage.h — C-ABI of libbloomstage.so, the MI355X-native per-stage BLOOM forward.
+ *
+ * Drop-in boundary for the reference's JNI stage library.  Every entry
+ * point below names the reference interface it replaces:
+ *
+ *   bs_init_stage      <- Java_..._Communication_createSession (native-lib.cpp:671-678)
+ *                         + SessionCache ctor (session_cache.h:26-35): load one module
+ *   bs_release         <- Java_..._Communication_releaseSession (native-lib.cpp:1290-1303)
+ *   bs_forward         <- runInferenceMasterResidual (native-lib.cpp:942-1034, header stage),
+ *                         runInferenceWorkerResidual (:1036-1194, middle stage),
+ *                         runInferenceWorkerResidualLastGeneration (:1368-1443, tail stage),
+ *                         all of which end in inference::run_inference (inference.cpp:145-218)
+ *   bs_reset_kv        <- (none: the reference has no KV cache; new sample == new slot)
+ *   bs_last_error      <- (none: the reference throws C++ exceptions across JNI,
+ *                         native-lib.cpp:986-988; here errors are status codes + this string)
+ *   bs_codec_*         <- utils::SerializeTensorVectorToBytes / DeserializeTensorVectorFromBytes
+ *                         (utils.cpp:124-264 / :266-368), byte-exact wire format
+ *   bs_serialize_int / bs_deserialize_int
+ *                      <- utils::SerializeInt / DeserializeInt (utils.cpp:11-25),
+ *                         Java_..._deserializeInt (native-lib.cpp:1445-1471)
+ *
+ * Conventions: no exceptions cross this ABI; every int-returning call returns BS_OK (0)
+ * or a negative bs_status and sets a thread-local message readable via bs_last_error().
+ * Plain pointers and sizes only.  Device pointers live on the stage's device.
+ */
+#ifndef BLOOMSTAGE_H
+#define BLOOMSTAGE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BS_ABI_VERSION 1
+
+typedef enum {
+  BS_OK = 0,
+  BS_ERR_INVALID = -1,   /* bad argument / shape outside the stage's capacity */
+  BS_ERR_DEVICE = -2,    /* HIP runtime error */
+  BS_ERR_OOM = -3,       /* device allocation failed */
+  BS_ERR_STATE = -4,     /* call not valid in the stage's current state */
+  BS_ERR_UNSUPPORTED = -5/* e.g. wire dtype the reference codec does not carry */
+} bs_status;
+
+/* Element types: values are ONNXTensorElementDataType (onnxruntime_c_api.h:175-191). */
+typedef enum {
+  BS_DT_FLOAT = 1, BS_DT_UINT8 = 2, BS_DT_INT8 = 3, BS_DT_UINT16 = 4, BS_DT_INT16 = 5,
+  BS_DT_INT32 = 6, BS_DT_INT64 = 7, BS_DT_BOOL = 9, BS_DT_DOUBLE = 11, BS_DT_UINT32 = 12,
+  BS_DT_UINT64 = 13, BS_DT_BFLOAT16 = 16
+} bs_dtype;
+
+typedef enum {
+  BS_WEIGHTS_SYNTHETIC = 0, /* repo generator (DESIGN.md "Synthetic weights"), built on device */
+  BS_WEIGHTS_HOST = 1       /* fp32 host buffer in canonical stage order (bs_stage_weight_count) */
+} bs_weight_source;
+
+typedef struct bs_stage_desc {
+  /* model (HF BloomConfig fields) */
+  int32_t hidden;        /* hidden_size */
+  int32_t n_head;        /* n_head */
+  int32_t n_layer;       /* n_layer (whole model) */
+  int32_t vocab;         /* vocab_size */
+  float ln_eps;          /* layer_norm_epsilon */
+  /* stage = contiguous layer range (server.py:893-905 assignment) */
+  int32_t layer_begin;
+  int32_t layer_end;     /* exclusive */
+  int32_t is_first;      /* owns word_embeddings + word_embeddings_layernorm */
+  int32_t is_last;       /* owns ln_f + tied lm_head + token pick */
+  /* storage */
+  int32_t dtype;         /* BS_DT_BFLOAT16 (weights + KV in bf16) or BS_DT_FLOAT */
+  int32_t device;        /* HIP device ordinal */
+  int32_t max_batch;     /* KV-cache rows (slots) */
+  int32_t max_ctx;       /* positions per KV row */
+  int32_t max_tokens;    /* max B*S per bs_forward call (0 -> max_batch*128) */
+  /* weights */
+  int32_t weight_source; /* bs_weight_source */
+  uint64_t seed;         /* BS_WEIGHTS_SYNTHETIC */
+  const float *host_weights;  /* BS_WEIGHTS_HOST */
+  uint64_t host_weight_count; /* floats in host_weights */
+  int32_t flags;         /* reserved, 0 */
+} bs_stage_desc;
+
+typedef struct bs_stage bs_stage;
+
+/* One forward call over B rows x S new tokens. */
+typedef struct bs_step {
+  int32_t batch;     /* B rows */
+  int32_t seq;       /* S new tokens per row */
+  int32_t slot;      /* first KV-cache row used by these B rows */
+  int32_t past_len;  /* positions already cached in those rows (same for all rows) */
+  int32_t flags;     /* BS_STEP_* */
+} bs_step;
+
+#define BS_STEP_HOST_IO 1  /* in/out/logits are host pointers (copied in/out, stream-synchronous) */
+#define BS_STEP_LOGITS 2   /* last stage also writes fp32 logits [B][vocab] of each row's last position */
+
+/* Create a stage on desc->device: allocates weights, KV cache and workspace in HBM. */
+int bs_init_stage(const bs_stage_desc *desc, bs_stage **out);
+
+/* Stage forward, stream-ordered on `stream` (hipStream_t, NULL = the stage's own stream).
+ *  in : first stage -> int32 token ids [B][S]; otherwise fp32 hidden [B][S][hidden]
+ *  out: last stage  -> int32 token ids [B] (greedy argmax of each row's last position);
+ *       otherwise fp32 hidden [B][S][hidden]
+ *  logits: fp32 [B][vocab] when step->flags & BS_STEP_LOGITS (last stage only), else NULL.
+ * Appends S positions to KV rows [slot, slot+B). Positions are past_len .. past_len+S-1. */
+int bs_forward(bs_stage *stage, const bs_step *step, const void *in, void *out, float *logits,
+               void *stream);
+
+/* Forget the cached positions of one KV row (slot), or of all rows when slot < 0. */
+int bs_reset_kv(bs_stage *stage, int32_t slot);
+
+void bs_release(bs_stage *stage);
+
+const char *bs_last_error(void);
+
+/* Introspection */
+int bs_stage_info(const bs_stage *stage, bs_stage_desc *out_desc, uint64_t *weight_bytes,
+                  uint64_t *kv_bytes, uint64_t *workspace_bytes);
+uint64_t bs_stage_weight_count(const bs_stage_desc *desc); /* fp32 count for BS_WEIGHTS_HOST */
+int bs_abi_version(void);
+/* Read back `count` weights starting at element `offset` of the canonical stage order
+ * (the BS_WEIGHTS_HOST layout) as fp32.  For verification of loaded/generated weights. */
+int bs_read_weights(const bs_stage *stage, uint64_t offset, uint64_t count, float *out);
+/* Synthetic prompt ids of the repo generator (DESIGN.md "Synthetic weights"): ids[i] for the
+ * flat index i of a [B][S] prompt, uniform over [0, vocab). */
+int bs_prompt_ids(uint64_t seed, int32_t n, int32_t vocab, int32_t *out);
+
+/* Profiling: time every launch of one kernel class with HIP events on the stage stream.
+ * kernel_class: 0 off, 1 weight GEMV (decode), 2 GEMM (prefill), 3 attention.
+ * bs_profile_read returns accumulated milliseconds, launch count and algorithmic bytes
+ * (or flops for class 2) since the last bs_profile_enable; it synchronizes the stream. */
+int bs_profile_enable(bs_stage *stage, int32_t kernel_class);
+int bs_profile_read(bs_stage *stage, double *total_ms, uint64_t *launches, double *algo_units);
+
+/* ---- Reference wire codec (utils.cpp:124-368): size_t n; per tensor {int32 dtype,
+ * size_t ndim, int64 dims[ndim], raw little-endian data}. size_t is 8 bytes (LP64). ---- */
+#define BS_CODEC_MAX_DIMS 8
+typedef struct bs_tensor_view {
+  int32_t dtype;                     /* bs_dtype */
+  int32_t ndim;
+  int64_t dims[BS_CODEC_MAX_DIMS];
+  const void *data;                  /* may be unaligned when it points into a wire buffer */
+} bs_tensor_view;
+
+/* Serialize n tensors. Returns the total byte count (also when out is NULL or too small:
+ * then nothing is written) or a negative bs_status. */
+int64_t bs_codec_serialize(const bs_tensor_view *tensors, int32_t n, void *out, uint64_t out_cap);
+/* Parse a wire buffer into zero-copy views. *n_out receives the tensor count; at most
+ * max_views are filled. Returns BS_OK or a negative bs_status (truncated / unsupported). */
+int bs_codec_deserialize(const void *bytes, uint64_t len, bs_tensor_view *views, int32_t max_views,
+                         int32_t *n_out);
+int64_t bs_dtype_size(int32_t dtype);
+/* 4-byte native (little-endian) int, as the tail stage returns a token id. */
+void bs_serialize_int(int32_t value, uint8_t out[4]);
+int bs_deserialize_int(const uint8_t *bytes, uint64_t len, int32_t *value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLOOMSTAGE_H */

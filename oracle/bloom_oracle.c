@@ -1,0 +1,320 @@
+/*
+ * oracle/bloom_oracle.c — TEST INFRASTRUCTURE: CPU restatement of one BLOOM pipeline
+ * stage forward.  Used only as the checker by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py.  Never linked into or called by the product path.
+ *
+ * What it restates:
+ *   The reference runs one ONNX sub-model per stage through ORT
+ *   (inference.cpp:145-218, Session::Run :207-215).  The arithmetic inside those ONNX
+ *   modules is HF BLOOM (the modules are exported from it by the absent util.model_card),
+ *   so the math below follows transformers' modeling_bloom.py:
+ *     - ALiBi slopes / positions  build_alibi_tensor (modeling_bloom.py:43-89)
+ *     - tanh-GELU                 bloom_gelu_forward (:111-121)
+ *     - attention                 BloomAttention.forward (:245-310): interleaved fused QKV
+ *                                 [heads,3,hd], scores = alibi + q.k/sqrt(hd), causal
+ *                                 mask, fp32 softmax, context, dense + bias, + residual
+ *     - MLP                       BloomMLP.forward (:325-340)
+ *     - block residual order      BloomBlock.forward (:359-403), residual = pre-LN input
+ *     - embedding + emb LN, ln_f  BloomModel.forward (:448-536); tied lm_head (:561-566)
+ *   The tail token pick is greedy argmax (first maximal index, like torch.argmax) instead
+ *   of the reference's non-deterministic top-k sampler (decoding.cpp:24-66); see
+ *   DESIGN.md "Token pick".
+ *
+ * Stage semantics = bs_forward() in include/bloomstage.h: first stage takes int32 ids
+ * [B,S], others fp32 hidden [B,S,h]; last stage emits int32 ids [B] (+ optional fp32
+ * logits [B,V] of the last position), others fp32 hidden [B,S,h].  KV cache rows
+ * [slot, slot+B) hold positions [0, past_len) on entry; S new positions are appended.
+ *
+ * bf16 mode emulates the device path's storage roundings exactly (weights, LN outputs
+ * feeding GEMMs, K/V cache, attention context, GELU output) while accumulating in fp32,
+ * so GPU-vs-oracle differences are accumulation-order only.
+ *
+ * Parity pinning: checked against transformers' BloomForCausalLM on CPU fp32 with the
+ * same generated weights (tests/golden/make_golden.py -> tests/golden/ fixtures,
+ * tests/test_oracle_golden.py).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <omp.h>
+
+#include "gen.h"
+
+typedef struct {
+  float *ln1_g, *ln1_b, *qkv_w, *qkv_b, *dense_w, *dense_b;
+  float *ln2_g, *ln2_b, *fc1_w, *fc1_b, *fc2_w, *fc2_b;
+} or_layer;
+
+typedef struct or_stage {
+  int h, nh, hd, nl, V;
+  float eps;
+  int lb, le, first, last, bf16;
+  int max_batch, max_ctx;
+  float *wemb, *emb_g, *emb_b, *lnf_g, *lnf_b;
+  or_layer *layers;
+  float *kv;      /* [L_s][2][max_batch][nh][max_ctx][hd] */
+  float *slopes;  /* [nh] */
+} or_stage;
+
+/* ---- ALiBi slopes, restating build_alibi_tensor (modeling_bloom.py:60-78) ---- */
+void or_alibi_slopes(int n_head, float *out) {
+  int cp2 = 1;
+  while (cp2 * 2 <= n_head) cp2 *= 2;
+  double base = pow(2.0, -pow(2.0, -(log2((double)cp2) - 3.0)));
+  float basef = (float)base;
+  for (int i = 0; i < cp2; i++) out[i] = (float)pow((double)basef, (double)(i + 1));
+  if (cp2 != n_head) {
+    double eb = pow(2.0, -pow(2.0, -(log2((double)(2 * cp2)) - 3.0)));
+    float ebf = (float)eb;
+    int rem = n_head - cp2 < cp2 ? n_head - cp2 : cp2;
+    for (int i = 0; i < rem; i++) out[cp2 + i] = (float)pow((double)ebf, (double)(2 * i + 1));
+  }
+}
+
+static float *gen_tensor(uint64_t seed, int layer, int tid, size_t n, int kind, int bf16) {
+  float *p = (float *)malloc(n * sizeof(float));
+  uint64_t key = gen_tensor_key(seed, layer, (uint32_t)tid);
+#pragma omp parallel for schedule(static)
+  for (size_t i = 0; i < n; i++) {
+    float v = gen_value(kind, key, (uint32_t)i);
+    p[i] = bf16 ? gen_bf16_round(v) : v;
+  }
+  return p;
+}
+
+/* exported for the generator-agreement tests */
+void or_gen_tensor(uint64_t seed, int layer, int tid, uint64_t n, float *out) {
+  int kind = layer < 0 ? gen_model_kind(tid) : gen_layer_kind(tid);
+  uint64_t key = gen_tensor_key(seed, layer, (uint32_t)tid);
+  for (uint64_t i = 0; i < n; i++) out[i] = gen_value(kind, key, (uint32_t)i);
+}
+
+void or_prompt_ids(uint64_t seed, int n, int vocab, int32_t *out) {
+  for (int i = 0; i < n; i++) out[i] = (int32_t)gen_prompt_id(seed, (uint32_t)i, (uint32_t)vocab);
+}
+
+void or_destroy(or_stage *s);
+
+or_stage *or_create(int hidden, int n_head, int n_layer, int vocab, float eps, int layer_begin,
+                    int layer_end, int is_first, int is_last, int bf16, int max_batch, int max_ctx,
+                    uint64_t seed) {
+  if (hidden <= 0 || n_head <= 0 || hidden % n_head || layer_begin < 0 || layer_end > n_layer ||
+      layer_begin > layer_end || max_batch <= 0 || max_ctx <= 0)
+    return NULL;
+  or_stage *s = (or_stage *)calloc(1, sizeof(or_stage));
+  s->h = hidden; s->nh = n_head; s->hd = hidden / n_head; s->nl = n_layer; s->V = vocab;
+  s->eps = eps; s->lb = layer_begin; s->le = layer_end; s->first = is_first; s->last = is_last;
+  s->bf16 = bf16; s->max_batch = max_batch; s->max_ctx = max_ctx;
+  size_t h = (size_t)hidden;
+  if (is_first || is_last) s->wemb = gen_tensor(seed, -1, GT_WEMB, (size_t)vocab * h, 0, bf16);
+  if (is_first) {
+    s->emb_g = gen_tensor(seed, -1, GT_EMB_G, h, 2, bf16);
+    s->emb_b = gen_tensor(seed, -1, GT_EMB_B, h, 3, bf16);
+  }
+  if (is_last) {
+    s->lnf_g = gen_tensor(seed, -1, GT_LNF_G, h, 2, bf16);
+    s->lnf_b = gen_tensor(seed, -1, GT_LNF_B, h, 3, bf16);
+  }
+  int L = layer_end - layer_begin;
+  s->layers = (or_layer *)calloc(L > 0 ? L : 1, sizeof(or_layer));
+  for (int i = 0; i < L; i++) {
+    int l = layer_begin + i;
+    or_layer *w = &s->layers[i];
+    size_t sz[GT_NUM_LAYER_TENSORS] = {h, h, 3 * h * h, 3 * h, h * h, h, h, h, 4 * h * h, 4 * h, 4 * h * h, h};
+    float **dst[GT_NUM_LAYER_TENSORS] = {&w->ln1_g, &w->ln1_b, &w->qkv_w, &w->qkv_b, &w->dense_w, &w->dense_b,
+                                         &w->ln2_g, &w->ln2_b, &w->fc1_w, &w->fc1_b, &w->fc2_w, &w->fc2_b};
+    for (int t = 0; t < GT_NUM_LAYER_TENSORS; t++)
+      *dst[t] = gen_tensor(seed, l, t, sz[t], gen_layer_kind(t), bf16);
+  }
+  size_t kvn = (size_t)(L > 0 ? L : 1) * 2 * max_batch * n_head * max_ctx * s->hd;
+  s->kv = (float *)calloc(kvn, sizeof(float));
+  s->slopes = (float *)malloc(sizeof(float) * n_head);
+  or_alibi_slopes(n_head, s->slopes);
+  if (!s->kv) { or_destroy(s); return NULL; }
+  return s;
+}
+
+void or_destroy(or_stage *s) {
+  if (!s) return;
+  free(s->wemb); free(s->emb_g); free(s->emb_b); free(s->lnf_g); free(s->lnf_b);
+  int L = s->le - s->lb;
+  for (int i = 0; i < L; i++) {
+    or_layer *w = &s->layers[i];
+    free(w->ln1_g); free(w->ln1_b); free(w->qkv_w); free(w->qkv_b); free(w->dense_w); free(w->dense_b);
+    free(w->ln2_g); free(w->ln2_b); free(w->fc1_w); free(w->fc1_b); free(w->fc2_w); free(w->fc2_b);
+  }
+  free(s->layers); free(s->kv); free(s->slopes); free(s);
+}
+
+static inline float rb(const or_stage *s, float v) { return s->bf16 ? gen_bf16_round(v) : v; }
+
+static int g_accum_double = 0; /* test knob: accumulate dot products in double */
+void or_set_accum_double(int on) { g_accum_double = on; }
+
+static float dotf(const float *a, const float *b, int K) {
+  if (g_accum_double) {
+    double d = 0.0;
+    for (int k = 0; k < K; k++) d += (double)a[k] * (double)b[k];
+    return (float)d;
+  }
+  float acc[16] = {0};
+  int k = 0;
+  for (; k + 16 <= K; k += 16)
+    for (int j = 0; j < 16; j++) acc[j] += a[k + j] * b[k + j];
+  float t = 0.f;
+  for (; k < K; k++) t += a[k] * b[k];
+  for (int w = 8; w >= 1; w >>= 1)
+    for (int j = 0; j < w; j++) acc[j] += acc[j + w];
+  return acc[0] + t;
+}
+
+/* LayerNorm over rows, HF nn.LayerNorm semantics (biased variance, eps inside sqrt). */
+static void layernorm(const float *x, float *y, int M, int K, const float *g, const float *b, float eps,
+                      int round_out, const or_stage *s) {
+#pragma omp parallel for schedule(static)
+  for (int m = 0; m < M; m++) {
+    const float *xr = x + (size_t)m * K;
+    double mean = 0, var = 0;
+    for (int k = 0; k < K; k++) mean += xr[k];
+    mean /= K;
+    for (int k = 0; k < K; k++) { double d = xr[k] - mean; var += d * d; }
+    var /= K;
+    float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    float mf = (float)mean;
+    for (int k = 0; k < K; k++) {
+      float v = (xr[k] - mf) * rstd * g[k] + b[k];
+      y[(size_t)m * K + k] = round_out ? rb(s, v) : v;
+    }
+  }
+}
+
+/* y[m][n] = x[m].W[n] + bias[n]  (nn.Linear with weight [out][in]) */
+static void linear(const float *x, const float *W, const float *bias, float *y, int M, int N, int K) {
+#pragma omp parallel for schedule(static)
+  for (int n = 0; n < N; n++) {
+    const float *wr = W + (size_t)n * K;
+    for (int m = 0; m < M; m++) {
+      float v = dotf(x + (size_t)m * K, wr, K);
+      y[(size_t)m * N + n] = bias ? v + bias[n] : v;
+    }
+  }
+}
+
+static inline float gelu_bloom(float x) {
+  /* bloom_gelu_forward (modeling_bloom.py:111-121), same evaluation order */
+  return x * 0.5f * (1.0f + tanhf(0.79788456f * x * (1.0f + 0.044715f * x * x)));
+}
+
+static float *kv_ptr(const or_stage *s, int li, int which, int row, int head, int pos) {
+  size_t idx = ((((size_t)li * 2 + which) * s->max_batch + row) * s->nh + head);
+  return s->kv + (idx * s->max_ctx + pos) * s->hd;
+}
+
+int or_forward(or_stage *s, int B, int S, int slot, int past_len, const void *in, void *out, float *logits) {
+  if (B <= 0 || S <= 0 || slot < 0 || slot + B > s->max_batch || past_len < 0 || past_len + S > s->max_ctx)
+    return -1;
+  const int h = s->h, nh = s->nh, hd = s->hd, M = B * S;
+  float *x = (float *)malloc(sizeof(float) * M * h);
+  float *xn = (float *)malloc(sizeof(float) * M * h);
+  float *a = (float *)malloc(sizeof(float) * M * h);
+  float *ctx = (float *)malloc(sizeof(float) * M * h);
+  float *qkv = (float *)malloc(sizeof(float) * M * 3 * h);
+  float *g = (float *)malloc(sizeof(float) * (size_t)M * 4 * h);
+
+  if (s->first) {
+    const int32_t *ids = (const int32_t *)in;
+    for (int m = 0; m < M; m++) {
+      int id = ids[m];
+      if (id < 0 || id >= s->V) { free(x); free(xn); free(a); free(ctx); free(qkv); free(g); return -2; }
+      memcpy(x + (size_t)m * h, s->wemb + (size_t)id * h, sizeof(float) * h);
+    }
+    layernorm(x, x, M, h, s->emb_g, s->emb_b, s->eps, 0, s);
+  } else {
+    memcpy(x, in, sizeof(float) * M * h);
+  }
+
+  const float inv_norm = 1.0f / sqrtf((float)hd);
+  int L = s->le - s->lb;
+  for (int li = 0; li < L; li++) {
+    or_layer *w = &s->layers[li];
+    layernorm(x, xn, M, h, w->ln1_g, w->ln1_b, s->eps, 1, s);
+    linear(xn, w->qkv_w, w->qkv_b, qkv, M, 3 * h, h);
+    /* fused qkv is [heads][3][hd] per token (modeling_bloom.py _reshape) */
+    for (int m = 0; m < M; m++) {
+      int b = m / S, t = m % S, pos = past_len + t;
+      for (int hh = 0; hh < nh; hh++) {
+        const float *base = qkv + (size_t)m * 3 * h + (size_t)hh * 3 * hd;
+        float *kd = kv_ptr(s, li, 0, slot + b, hh, pos), *vd = kv_ptr(s, li, 1, slot + b, hh, pos);
+        for (int d = 0; d < hd; d++) { kd[d] = rb(s, base[hd + d]); vd[d] = rb(s, base[2 * hd + d]); }
+      }
+    }
+#pragma omp parallel for collapse(2) schedule(dynamic)
+    for (int b = 0; b < B; b++)
+      for (int hh = 0; hh < nh; hh++) {
+        int nk_max = past_len + S;
+        float *sc = (float *)malloc(sizeof(float) * nk_max);
+        for (int t = 0; t < S; t++) {
+          int m = b * S + t, nk = past_len + t + 1; /* causal: keys 0..pos */
+          const float *q = qkv + (size_t)m * 3 * h + (size_t)hh * 3 * hd;
+          float mx = -INFINITY;
+          for (int j = 0; j < nk; j++) {
+            float qk = dotf(q, kv_ptr(s, li, 0, slot + b, hh, j), hd);
+            float v = s->slopes[hh] * (float)j + inv_norm * qk; /* alibi.baddbmm(beta=1, alpha=inv_norm) */
+            sc[j] = v;
+            if (v > mx) mx = v;
+          }
+          float sum = 0.f;
+          for (int j = 0; j < nk; j++) { sc[j] = expf(sc[j] - mx); sum += sc[j]; }
+          float inv = 1.0f / sum;
+          float *o = ctx + (size_t)m * h + (size_t)hh * hd;
+          for (int d = 0; d < hd; d++) o[d] = 0.f;
+          for (int j = 0; j < nk; j++) {
+            const float *vr = kv_ptr(s, li, 1, slot + b, hh, j);
+            float p = sc[j] * inv;
+            for (int d = 0; d < hd; d++) o[d] += p * vr[d];
+          }
+          for (int d = 0; d < hd; d++) o[d] = rb(s, o[d]);
+        }
+        free(sc);
+      }
+    /* a = x + dense(ctx) */
+    linear(ctx, w->dense_w, w->dense_b, a, M, h, h);
+    for (size_t i = 0; i < (size_t)M * h; i++) a[i] = a[i] + x[i];
+    layernorm(a, xn, M, h, w->ln2_g, w->ln2_b, s->eps, 1, s);
+    linear(xn, w->fc1_w, w->fc1_b, g, M, 4 * h, h);
+    for (size_t i = 0; i < (size_t)M * 4 * h; i++) g[i] = rb(s, gelu_bloom(g[i]));
+    linear(g, w->fc2_w, w->fc2_b, x, M, h, 4 * h);
+    for (size_t i = 0; i < (size_t)M * h; i++) x[i] = x[i] + a[i];
+  }
+
+  if (s->last) {
+    /* ln_f on the last position of each row, tied lm_head, argmax */
+    for (int b = 0; b < B; b++)
+      memcpy(a + (size_t)b * h, x + ((size_t)b * S + S - 1) * h, sizeof(float) * h);
+    layernorm(a, xn, B, h, s->lnf_g, s->lnf_b, s->eps, 1, s);
+    float *lg = logits ? logits : (float *)malloc(sizeof(float) * (size_t)B * s->V);
+    linear(xn, s->wemb, NULL, lg, B, s->V, h);
+    int32_t *tok = (int32_t *)out;
+    for (int b = 0; b < B; b++) {
+      const float *r = lg + (size_t)b * s->V;
+      int best = 0;
+      for (int v = 1; v < s->V; v++) if (r[v] > r[best]) best = v;
+      tok[b] = best;
+    }
+    if (!logits) free(lg);
+  } else {
+    memcpy(out, x, sizeof(float) * M * h);
+  }
+  free(x); free(xn); free(a); free(ctx); free(qkv); free(g);
+  return 0;
+}
+
+/* Copy of one KV row for tests: which 0=K 1=V, layer index local to the stage. */
+int or_read_kv(const or_stage *s, int li, int which, int row, int head, int pos, float *out) {
+  if (li < 0 || li >= s->le - s->lb) return -1;
+  memcpy(out, kv_ptr(s, li, which, row, head, pos), sizeof(float) * s->hd);
+  return 0;
+}
+
+int or_num_threads(void) { return omp_get_max_threads(); }

@@ -1,0 +1,100 @@
+"""oracle/oracle.py — TEST INFRASTRUCTURE: ctypes loader for the CPU checker
+(oracle/liboracle.so, built by oracle/Makefile).  Only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg import this; the product path never does.
+"""
+import ctypes
+import os
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle` (or __graft_entry__.build())")
+        L = ctypes.CDLL(path)
+        L.or_create.restype = ctypes.c_void_p
+        L.or_create.argtypes = [ctypes.c_int] * 4 + [ctypes.c_float] + [ctypes.c_int] * 7 + [ctypes.c_uint64]
+        L.or_destroy.argtypes = [ctypes.c_void_p]
+        L.or_forward.restype = ctypes.c_int
+        L.or_forward.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 4 + [ctypes.c_void_p] * 3
+        L.or_gen_tensor.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p]
+        L.or_prompt_ids.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.or_alibi_slopes.argtypes = [ctypes.c_int, ctypes.c_void_p]
+        L.or_read_kv.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p]
+        L.or_num_threads.restype = ctypes.c_int
+        L.or_set_accum_double.argtypes = [ctypes.c_int]
+        _LIB = L
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def gen_tensor(seed, layer, tid, n):
+    out = np.empty(n, dtype=np.float32)
+    lib().or_gen_tensor(seed, layer, tid, n, _p(out))
+    return out
+
+
+def prompt_ids(seed, batch, seq, vocab):
+    out = np.empty(batch * seq, dtype=np.int32)
+    lib().or_prompt_ids(seed, batch * seq, vocab, _p(out))
+    return out.reshape(batch, seq)
+
+
+def alibi_slopes(n_head):
+    out = np.empty(n_head, dtype=np.float32)
+    lib().or_alibi_slopes(n_head, _p(out))
+    return out
+
+
+def num_threads():
+    return lib().or_num_threads()
+
+
+class OracleStage:
+    """CPU checker for one pipeline stage; same call semantics as the product Stage."""
+
+    def __init__(self, hidden, n_head, n_layer, vocab, layer_begin, layer_end, *, bf16=False,
+                 max_batch=1, max_ctx=64, seed=0, eps=1e-5, is_first=None, is_last=None):
+        self.hidden, self.vocab = hidden, vocab
+        self.is_first = layer_begin == 0 if is_first is None else is_first
+        self.is_last = layer_end == n_layer if is_last is None else is_last
+        self.h = lib().or_create(hidden, n_head, n_layer, vocab, eps, layer_begin, layer_end,
+                                 int(self.is_first), int(self.is_last), int(bf16), max_batch, max_ctx, seed)
+        if not self.h:
+            raise ValueError("or_create failed (bad stage description)")
+
+    def forward(self, x, B, S, slot=0, past_len=0, want_logits=False):
+        if self.is_first:
+            x = np.ascontiguousarray(x, dtype=np.int32).reshape(B, S)
+        else:
+            x = np.ascontiguousarray(x, dtype=np.float32).reshape(B, S, self.hidden)
+        logits = np.empty((B, self.vocab), dtype=np.float32) if (self.is_last and want_logits) else None
+        out = np.empty(B, dtype=np.int32) if self.is_last else np.empty((B, S, self.hidden), dtype=np.float32)
+        rc = lib().or_forward(self.h, B, S, slot, past_len, _p(x), _p(out), _p(logits))
+        if rc != 0:
+            raise ValueError(f"or_forward failed rc={rc}")
+        return (out, logits) if want_logits else out
+
+    def read_kv(self, layer_local, which, row, head, pos, head_dim):
+        out = np.empty(head_dim, dtype=np.float32)
+        lib().or_read_kv(self.h, layer_local, which, row, head, pos, _p(out))
+        return out
+
+    def close(self):
+        if self.h:
+            lib().or_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
