@@ -48,3 +48,13 @@ __device__ __forceinline__ uint32_t f32_order_key(float f) {
   uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
+
+// 8 consecutive elements kept in their storage type (bf16: 4 VGPRs) until used.
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16> { typedef u16x8 type; };
+template <> struct Raw8<float> { typedef f32x8 type; };
+__device__ __forceinline__ void raw_load(const bf16* p, u16x8& r) { r = *reinterpret_cast<const u16x8*>(p); }
+__device__ __forceinline__ void raw_load(const float* p, f32x8& r) { r = *reinterpret_cast<const f32x8*>(p); }
+__device__ __forceinline__ float raw_get(const u16x8& r, int j) { return __uint_as_float(((uint32_t)r[j]) << 16); }
+__device__ __forceinline__ float raw_get(const f32x8& r, int j) { return r[j]; }

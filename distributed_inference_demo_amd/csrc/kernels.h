@@ -46,6 +46,11 @@ void launch_layernorm(int is_bf16, const void* x, const int* ids, int row_stride
 void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int K, const Epi& ep,
                    hipStream_t s);
 
+// LayerNorm(x rows) followed by a weight GEMM; fused into one kernel on the bf16 decode path.
+void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offset, const void* gamma,
+                      const void* beta, float eps, void* xn_scratch, const void* W, int M, int N, int K,
+                      const Epi& ep, hipStream_t s);
+
 // Attention over the KV cache for B rows x S new queries per row (causal, ALiBi).
 struct AttnArgs {
   const float* q;      // [B*S][hidden] fp32
@@ -61,7 +66,7 @@ struct AttnArgs {
   float* part_acc;     // workspace [B][n_head][max_chunks][head_dim]
   float* part_ml;      // workspace [B][n_head][max_chunks][2]
   int max_chunks;
-  int chunk;           // positions per split-K chunk (decode)
+  int chunk;           // positions per chunk (decode) = 64
 };
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s);
 size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, int* max_chunks, int* chunk);

@@ -13,6 +13,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 // ------------------------------------------------------------------------------------
 // Synthetic weights: device twin of oracle/gen.h (DESIGN.md "Synthetic weights").
 // ------------------------------------------------------------------------------------
@@ -38,6 +40,9 @@ __device__ __forceinline__ float d_gen_value(int kind, uint64_t key, uint64_t ke
   int s = 2 * (int)(d_bits(key, i) >> 8) - 16777215;
   if (kind == 1) return __fmul_rn((float)s, 0x1.47ae14p-30f);
   float t = __fmul_rn((float)s, 0x1.99999ap-28f);
+  // gamma = 1 + s*c must round twice (like the C and numpy twins): the empty asm makes t
+  // opaque so the add cannot be fused into a v_fma_f32.
+  asm volatile("" : "+v"(t));
   return kind == 2 ? __fadd_rn(1.0f, t) : t;
 }
 
@@ -148,34 +153,48 @@ __device__ __forceinline__ void argmax_tile16(const Epi& e, int m, int n, float 
   if (valid && e.logits) e.logits[(size_t)m * e.ldo + n] = v;
 }
 
-template <typename T>
+template <typename T, int KIND>
 __device__ __forceinline__ void epi_store(const Epi& e, int m, int n, float v) {
-  switch (e.kind) {
-    case EPI_QKV: {
-      v += to_f32(((const T*)e.bias)[n]);
-      const int three = 3 * e.head_dim;
-      const int head = n / three, r = n - head * three, which = r / e.head_dim, d = r - which * e.head_dim;
-      if (which == 0) {
-        e.q_out[(size_t)m * e.hidden + head * e.head_dim + d] = v;
-      } else {
-        const int b = m / e.seq, t = m - b * e.seq;
-        const int past = e.past_dev ? *e.past_dev : e.past;
-        const size_t idx = (((size_t)(e.slot + b) * e.n_head + head) * e.max_ctx + past + t) * e.head_dim + d;
-        T* c = (T*)(which == 1 ? e.k_cache : e.v_cache);
-        c[idx] = from_f32<T>(v);
-      }
-      break;
+  if constexpr (KIND == EPI_QKV) {
+    v += to_f32(((const T*)e.bias)[n]);
+    const int three = 3 * e.head_dim;
+    const int head = n / three, r = n - head * three, which = r / e.head_dim, d = r - which * e.head_dim;
+    if (which == 0) {
+      e.q_out[(size_t)m * e.hidden + head * e.head_dim + d] = v;
+    } else {
+      const int b = m / e.seq, t = m - b * e.seq;
+      const int past = e.past_dev ? *e.past_dev : e.past;
+      const size_t idx = (((size_t)(e.slot + b) * e.n_head + head) * e.max_ctx + past + t) * e.head_dim + d;
+      T* c = (T*)(which == 1 ? e.k_cache : e.v_cache);
+      c[idx] = from_f32<T>(v);
     }
-    case EPI_RESID: {
-      const size_t i = (size_t)m * e.ldo + n;
-      e.out_f32[i] = (v + to_f32(((const T*)e.bias)[n])) + e.resid[i];
-      break;
-    }
-    case EPI_GELU: {
-      ((T*)e.out_act)[(size_t)m * e.ldo + n] = from_f32<T>(gelu_bloom(v + to_f32(((const T*)e.bias)[n])));
-      break;
-    }
-    default: break;
+  } else if constexpr (KIND == EPI_RESID) {
+    const size_t i = (size_t)m * e.ldo + n;
+    e.out_f32[i] = (v + to_f32(((const T*)e.bias)[n])) + e.resid[i];
+  } else if constexpr (KIND == EPI_GELU) {
+    ((T*)e.out_act)[(size_t)m * e.ldo + n] = from_f32<T>(gelu_bloom(v + to_f32(((const T*)e.bias)[n])));
+  }
+}
+
+// Apply the epilogue of compile-time kind K to one element (argmax needs all 64 lanes).
+template <typename T, int K>
+__device__ __forceinline__ void epi_apply(const Epi& ep, int m, int n, float v, bool valid, int ntiles) {
+  if constexpr (K == EPI_ARGMAX) argmax_tile16(ep, m, n, v, valid, ntiles);
+  else if (valid) epi_store<T, K>(ep, m, n, v);
+}
+
+template <int V> struct EpiKindC { static constexpr int value = V; };
+
+// Call f(EpiKindC<kind>) so the epilogue kind is a compile-time constant inside f: each kind's
+// loop nest then unrolls on its own (a runtime switch inside an unrolled accumulator loop
+// stops the unrolling and sends the accumulators to scratch).
+template <typename F>
+__device__ __forceinline__ void epi_dispatch(int kind, F&& f) {
+  switch (kind) {
+    case EPI_QKV: f(EpiKindC<EPI_QKV>{}); break;
+    case EPI_RESID: f(EpiKindC<EPI_RESID>{}); break;
+    case EPI_GELU: f(EpiKindC<EPI_GELU>{}); break;
+    default: f(EpiKindC<EPI_ARGMAX>{}); break;
   }
 }
 
@@ -185,45 +204,162 @@ __device__ __forceinline__ void epi_store(const Epi& e, int m, int n, float v) {
 // lane, U k-steps in flight) and runs one v_mfma_f32_16x16x32_bf16 per k-step and m-tile
 // with A = W tile (rows = n), B = X^T (cols = m).  Partial tiles meet in LDS.
 // ------------------------------------------------------------------------------------
-template <int WAVES, int MT, int U>
+// LN variant (LN = true, M <= 8): X is the fp32 residual stream; the block computes the
+// LayerNorm statistics of its M rows (two passes, L2-resident) while its first U weight
+// loads are in flight, writes the normalised bf16 rows to LDS, and reads B fragments there.
+struct LnArgs {
+  const float* x;     // fp32 rows; source row of m = m * row_stride + row_offset
+  int row_stride, row_offset;
+  const bf16* gamma;
+  const bf16* beta;
+  float eps;
+};
+
+// NT: non-temporal weight loads; PF: prefetch the next U weight steps before this step's MFMAs.
+template <int WAVES, int MT, int U, bool LN, int NT = 1, int PF = 1>
 __global__ __launch_bounds__(WAVES * 64) void gemv_mfma_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
-                                                               int M, int N, int K, Epi ep) {
-  __shared__ float red[WAVES][MT * 16][17];
+                                                               LnArgs ln, int M, int N, int K, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float (*red)[MT * 16][17] = reinterpret_cast<float (*)[MT * 16][17]>(smem);
+  bf16* xs = reinterpret_cast<bf16*>(smem + sizeof(float) * WAVES * MT * 16 * 17);  // LN: [M][K]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16;
   const bf16* wp = W + (size_t)min(n0 + r, N - 1) * K + g * 8;
-  const bf16* xp[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; mt++) xp[mt] = X + (size_t)min(mt * 16 + r, M - 1) * K + g * 8;
   const int ksteps = K >> 5;
   const int per = (ksteps + WAVES - 1) / WAVES;
   const int s0 = w * per, s1 = min(ksteps, s0 + per);
+  auto wload = [&](int ss) -> bf16x8 {
+    const bf16x8* p = reinterpret_cast<const bf16x8*>(wp + (size_t)ss * 32);
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+  };
+  bf16x8 a[U];
+  if (PF && s0 < s1) {
+#pragma unroll
+    for (int u = 0; u < U; u++) a[u] = wload(min(s0 + u, s1 - 1));
+  }
+  const bf16* xp[MT];
+  if constexpr (LN) {
+    // ---- LayerNorm prologue (nn.LayerNorm: biased variance, eps inside the sqrt)
+    float* st = &red[0][0][0];  // reuse: [2][8] stats + [WAVES][8] partials
+    float part[8];
+    const int nthr = WAVES * 64;
+#pragma unroll
+    for (int m = 0; m < 8; m++) part[m] = 0.f;
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      if (m < M) {
+        const float* xr = ln.x + ((size_t)m * ln.row_stride + ln.row_offset) * K;
+        float acc = 0.f;
+        for (int k = threadIdx.x * 4; k < K; k += nthr * 4) {
+          const float4 v = *reinterpret_cast<const float4*>(xr + k);
+          acc += (v.x + v.y) + (v.z + v.w);
+        }
+        part[m] = wave_sum(acc);
+      }
+    }
+    float* wp_part = st + 16;
+    if (lane == 0) {
+#pragma unroll
+      for (int m = 0; m < 8; m++)
+        if (m < M) wp_part[w * 8 + m] = part[m];
+    }
+    __syncthreads();
+    if (threadIdx.x < M) {
+      float t = 0.f;
+      for (int ww = 0; ww < WAVES; ww++) t += wp_part[ww * 8 + threadIdx.x];
+      st[threadIdx.x] = t / (float)K;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      if (m < M) {
+        const float* xr = ln.x + ((size_t)m * ln.row_stride + ln.row_offset) * K;
+        const float mean = st[m];
+        float acc = 0.f;
+        for (int k = threadIdx.x * 4; k < K; k += nthr * 4) {
+          const float4 v = *reinterpret_cast<const float4*>(xr + k);
+          const float d0 = v.x - mean, d1 = v.y - mean, d2 = v.z - mean, d3 = v.w - mean;
+          acc += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+        }
+        part[m] = wave_sum(acc);
+      }
+    }
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+      for (int m = 0; m < 8; m++)
+        if (m < M) wp_part[w * 8 + m] = part[m];
+    }
+    __syncthreads();
+    if (threadIdx.x < M) {
+      float t = 0.f;
+      for (int ww = 0; ww < WAVES; ww++) t += wp_part[ww * 8 + threadIdx.x];
+      st[8 + threadIdx.x] = 1.0f / sqrtf(t / (float)K + ln.eps);
+    }
+    __syncthreads();
+    for (int m = 0; m < M; m++) {
+      const float* xr = ln.x + ((size_t)m * ln.row_stride + ln.row_offset) * K;
+      const float mean = st[m], rstd = st[8 + m];
+      for (int k = threadIdx.x * 8; k < K; k += nthr * 8) {
+        float xv[8], gv[8], bv[8];
+        load8(xr + k, xv);
+        load8(ln.gamma + k, gv);
+        load8(ln.beta + k, bv);
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = (bf16)((xv[j] - mean) * rstd * gv[j] + bv[j]);
+        *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + k) = o;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++) xp[mt] = xs + (size_t)min(mt * 16 + r, M - 1) * K + g * 8;
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++) xp[mt] = X + (size_t)min(mt * 16 + r, M - 1) * K + g * 8;
+  }
   f32x4 acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; mt++) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  int s = s0;
-  for (; s + U <= s1; s += U) {
-    bf16x8 a[U], b[MT][U];
+  // U k-steps per iteration, always fully unrolled: the steps past s1 re-load step s1-1
+  // (an L1/L2 hit) and contribute a zeroed B fragment, so a short K range still keeps U
+  // weight loads in flight instead of falling into a one-load-at-a-time remainder loop.
+  // The next iteration's weights are loaded before this iteration's MFMAs.
+  const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  for (int s = s0; s < s1; s += U) {
+    if constexpr (!PF) {
 #pragma unroll
-    for (int u = 0; u < U; u++) a[u] = *reinterpret_cast<const bf16x8*>(wp + (size_t)(s + u) * 32);
+      for (int u = 0; u < U; u++) a[u] = wload(min(s + u, s1 - 1));
+    }
+    bf16x8 b[MT][U];
 #pragma unroll
     for (int mt = 0; mt < MT; mt++)
 #pragma unroll
-      for (int u = 0; u < U; u++) b[mt][u] = *reinterpret_cast<const bf16x8*>(xp[mt] + (size_t)(s + u) * 32);
+      for (int u = 0; u < U; u++) {
+        const int ss = min(s + u, s1 - 1);
+        b[mt][u] = *reinterpret_cast<const bf16x8*>(xp[mt] + (size_t)ss * 32);
+      }
+    bf16x8 an[U];
+    const bool more = PF && s + U < s1;
+    if (more) {
 #pragma unroll
-    for (int u = 0; u < U; u++)
+      for (int u = 0; u < U; u++) an[u] = wload(min(s + U + u, s1 - 1));
+    }
 #pragma unroll
-      for (int mt = 0; mt < MT; mt++) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[mt][u], acc[mt], 0, 0, 0);
-  }
-  for (; s < s1; ++s) {
-    bf16x8 a = *reinterpret_cast<const bf16x8*>(wp + (size_t)s * 32);
+    for (int u = 0; u < U; u++) {
+      const bool live = s + u < s1;
 #pragma unroll
-    for (int mt = 0; mt < MT; mt++) {
-      bf16x8 b = *reinterpret_cast<const bf16x8*>(xp[mt] + (size_t)s * 32);
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[mt], 0, 0, 0);
+      for (int mt = 0; mt < MT; mt++)
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], live ? b[mt][u] : zero8, acc[mt], 0, 0, 0);
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < U; u++) a[u] = an[u];
     }
   }
+  if constexpr (LN) __syncthreads();  // red aliases the stats scratch
   // D[row = 4g+i (n)][col = r (m)]
 #pragma unroll
   for (int mt = 0; mt < MT; mt++)
@@ -231,16 +367,189 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_mfma_kernel(const bf16* __res
     for (int i = 0; i < 4; i++) red[w][mt * 16 + r][4 * g + i] = acc[mt][i];
   __syncthreads();
   const int ntiles = (N + 15) >> 4;
-  for (int t = threadIdx.x; t < MT * 256; t += WAVES * 64) {
-    const int ml = t >> 4, nl = t & 15;
-    float v = 0.f;
+  epi_dispatch(ep.kind, [&](auto kc) {
+    constexpr int EK = decltype(kc)::value;
+    for (int t = threadIdx.x; t < MT * 256; t += WAVES * 64) {
+      const int ml = t >> 4, nl = t & 15;
+      float v = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < WAVES; ww++) v += red[ww][ml][nl];
-    const int m = ml, n = n0 + nl;
-    const bool valid = m < M && n < N;
-    if (ep.kind == EPI_ARGMAX) argmax_tile16(ep, m, n, v, valid, ntiles);
-    else if (valid) epi_store<bf16>(ep, m, n, v);
+      for (int ww = 0; ww < WAVES; ww++) v += red[ww][ml][nl];
+      const int n = n0 + nl;
+      epi_apply<bf16, EK>(ep, ml, n, v, ml < M && n < N, ntiles);
+    }
+  });
+}
+
+// ------------------------------------------------------------------------------------
+// gemv_rows: decode GEMV for M <= MM <= 4.  Each wave owns R consecutive weight rows and streams
+// them whole: every load instruction reads 1 KB contiguous (64 lanes x 16 B of one row), U
+// 512-column chunks per row in flight.  Dot products on v_dot2c_f32_bf16 against x (bf16, from
+// LDS for the LN variant, which normalises the rows there, else from global/L1).  Partial sums
+// per lane are reduced across the wave at the end.  Small blocks (4 waves) and one wave per
+// 1-4 rows give every CU several blocks, so no wave-quantisation tail on N = h GEMVs.
+// ------------------------------------------------------------------------------------
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float acc) {
+  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[0], a[1]}, (bf16x2){b[0], b[1]}, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[2], a[3]}, (bf16x2){b[2], b[3]}, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[4], a[5]}, (bf16x2){b[4], b[5]}, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[6], a[7]}, (bf16x2){b[6], b[7]}, acc, false);
+  return acc;
+}
+
+// LayerNorm of M <= 8 rows into LDS (bf16), 256 threads.  nn.LayerNorm semantics.
+__device__ __forceinline__ void ln_rows_to_lds(const LnArgs& ln, int M, int K, bf16* xs, float* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* st = scratch;           // [0..7] mean, [8..15] rstd
+  float* wp_part = scratch + 16; // [4 waves][8]
+  float part[8];
+#pragma unroll
+  for (int m = 0; m < 8; m++) {
+    part[m] = 0.f;
+    if (m < M) {
+      const float* xr = ln.x + ((size_t)m * ln.row_stride + ln.row_offset) * K;
+      float acc = 0.f;
+      for (int k = threadIdx.x * 4; k < K; k += 1024) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + k);
+        acc += (v.x + v.y) + (v.z + v.w);
+      }
+      part[m] = wave_sum(acc);
+    }
   }
+  if (lane == 0) {
+#pragma unroll
+    for (int m = 0; m < 8; m++) if (m < M) wp_part[w * 8 + m] = part[m];
+  }
+  __syncthreads();
+  if (threadIdx.x < M) st[threadIdx.x] = (wp_part[threadIdx.x] + wp_part[8 + threadIdx.x] + wp_part[16 + threadIdx.x] +
+                                          wp_part[24 + threadIdx.x]) / (float)K;
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < 8; m++) {
+    if (m < M) {
+      const float* xr = ln.x + ((size_t)m * ln.row_stride + ln.row_offset) * K;
+      const float mean = st[m];
+      float acc = 0.f;
+      for (int k = threadIdx.x * 4; k < K; k += 1024) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + k);
+        const float d0 = v.x - mean, d1 = v.y - mean, d2 = v.z - mean, d3 = v.w - mean;
+        acc += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+      }
+      part[m] = wave_sum(acc);
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int m = 0; m < 8; m++) if (m < M) wp_part[w * 8 + m] = part[m];
+  }
+  __syncthreads();
+  if (threadIdx.x < M) {
+    const float t = wp_part[threadIdx.x] + wp_part[8 + threadIdx.x] + wp_part[16 + threadIdx.x] + wp_part[24 + threadIdx.x];
+    st[8 + threadIdx.x] = 1.0f / sqrtf(t / (float)K + ln.eps);
+  }
+  __syncthreads();
+  for (int m = 0; m < M; m++) {
+    const float* xr = ln.x + ((size_t)m * ln.row_stride + ln.row_offset) * K;
+    const float mean = st[m], rstd = st[8 + m];
+    for (int k = threadIdx.x * 8; k < K; k += 2048) {
+      float xv[8], gv[8], bv[8];
+      load8(xr + k, xv);
+      load8(ln.gamma + k, gv);
+      load8(ln.beta + k, bv);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; j++) o[j] = (bf16)((xv[j] - mean) * rstd * gv[j] + bv[j]);
+      *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + k) = o;
+    }
+  }
+  __syncthreads();
+}
+
+template <int R, int MM, int U, bool LN>
+__global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
+                                                        LnArgs ln, int M, int N, int K, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* scratch = reinterpret_cast<float*>(smem);                  // 64 floats
+  bf16* xs = reinterpret_cast<bf16*>(smem + 256);                    // LN: [M][K]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n0 = (blockIdx.x * 4 + w) * R;
+  const bf16* wr[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) wr[r] = W + (size_t)min(n0 + r, N - 1) * K;
+  const bf16* xg;
+  int xstride;
+  if constexpr (LN) {
+    ln_rows_to_lds(ln, M, K, xs, scratch);
+    xg = xs; xstride = K;
+  } else {
+    xg = X; xstride = K;
+  }
+  float acc[R][MM];
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int m = 0; m < MM; m++) acc[r][m] = 0.f;
+  const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  for (int kb = 0; kb < K; kb += 512 * U) {
+    bf16x8 wv[U][R];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int k = min(kb + u * 512 + lane * 8, K - 8);
+#pragma unroll
+      for (int r = 0; r < R; r++) wv[u][r] = *reinterpret_cast<const bf16x8*>(wr[r] + k);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int kk = kb + u * 512 + lane * 8;
+      const bool live = kk < K;
+      const int k = min(kk, K - 8);
+#pragma unroll
+      for (int m = 0; m < MM; m++) {
+        bf16x8 xv = *reinterpret_cast<const bf16x8*>(xg + (size_t)min(m, M - 1) * xstride + k);
+        xv = live ? xv : zero8;
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r][m] = dot8(wv[u][r], xv, acc[r][m]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int m = 0; m < MM; m++) acc[r][m] = wave_sum(acc[r][m]);
+  epi_dispatch(ep.kind, [&](auto kc) {
+    constexpr int EK = decltype(kc)::value;
+    if constexpr (EK == EPI_ARGMAX) {
+      // R = 4, 4 waves: a block owns one 16-column tile; lane (4*w + r) holds column n0+r
+      float* tv = scratch;  // [16][MM] values
+      __syncthreads();
+      if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+          for (int m = 0; m < MM; m++) tv[(w * R + r) * MM + m] = acc[r][m];
+      }
+      __syncthreads();
+      if (threadIdx.x < 64) {
+        const int col = threadIdx.x & 15, m = threadIdx.x >> 4;  // 4 rows of 16 lanes: m < 4
+        const int n = blockIdx.x * 16 + col;
+        const float v = m < MM ? tv[col * MM + (m < MM ? m : 0)] : 0.f;
+        argmax_tile16(ep, m, n, v, m < M && n < N, (N + 15) >> 4);
+      }
+    } else {
+      if (lane < R * MM) {
+        // lane j = r * MM + m takes (row r, token m); static register selection
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+          for (int m = 0; m < MM; m++) v = (lane == r * MM + m) ? acc[r][m] : v;
+        const int r = lane / MM, m = lane % MM, n = n0 + r;
+        if (m < M && n < N) epi_store<bf16, EK>(ep, m, n, v);
+      }
+    }
+  });
 }
 
 // ------------------------------------------------------------------------------------
@@ -322,18 +631,19 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(const bf16* __restrict__
     cur ^= 1;
   }
   const int ntiles = (N + 15) >> 4;
+  epi_dispatch(ep.kind, [&](auto kc) {
+    constexpr int EK = decltype(kc)::value;
 #pragma unroll
-  for (int i = 0; i < TM; i++)
+    for (int i = 0; i < TM; i++)
 #pragma unroll
-    for (int j = 0; j < TN; j++)
+      for (int j = 0; j < TN; j++)
 #pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const int m = m0 + wm * (BM / 2) + i * 16 + 4 * g + e;
-        const int n = n0 + wn * (BN / 2) + j * 16 + r;
-        const bool valid = m < M && n < N;
-        if (ep.kind == EPI_ARGMAX) argmax_tile16(ep, m, n, acc[i][j][e], valid, ntiles);
-        else if (valid) epi_store<bf16>(ep, m, n, acc[i][j][e]);
-      }
+        for (int e = 0; e < 4; e++) {
+          const int m = m0 + wm * (BM / 2) + i * 16 + 4 * g + e;
+          const int n = n0 + wn * (BN / 2) + j * 16 + r;
+          epi_apply<bf16, EK>(ep, m, n, acc[i][j][e], m < M && n < N, ntiles);
+        }
+  });
 }
 
 // ------------------------------------------------------------------------------------
@@ -356,14 +666,83 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     __syncthreads();
   }
   const int m = m0 + ty, n = n0 + tx;
-  const bool valid = m < M && n < N;
-  if (ep.kind == EPI_ARGMAX) argmax_tile16(ep, m, n, acc, valid, (N + 15) >> 4);
-  else if (valid) epi_store<float>(ep, m, n, acc);
+  epi_dispatch(ep.kind, [&](auto kc) {
+    epi_apply<float, decltype(kc)::value>(ep, m, n, acc, m < M && n < N, (N + 15) >> 4);
+  });
 }
 
-template <int WAVES, int MT>
-static void gemv_launch(const bf16* X, const bf16* W, int M, int N, int K, const Epi& ep, hipStream_t s) {
-  gemv_mfma_kernel<WAVES, MT, 8><<<(N + 15) / 16, WAVES * 64, 0, s>>>(W, X, M, N, K, ep);
+static bool gemv_rows_disabled() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("BS_GEMV_MFMA"); v = (e && *e && *e != '0') ? 1 : 0; }
+  return v == 1;
+}
+
+template <int WAVES, int MT, bool LN>
+static void gemv_launch(const bf16* X, const LnArgs& ln, const bf16* W, int M, int N, int K, const Epi& ep,
+                        hipStream_t s) {
+  size_t shm = sizeof(float) * WAVES * MT * 16 * 17;
+  if (LN) shm += (size_t)M * K * sizeof(bf16);
+  // U = 4, plain (not non-temporal) loads, no software prefetch: the fastest variant in the
+  // tools/gemv_bench.hip A/B (profiles/r01_gemv_bench.log)
+  gemv_mfma_kernel<WAVES, MT, 4, LN, 0, 0><<<(N + 15) / 16, WAVES * 64, shm, s>>>(W, X, ln, M, N, K, ep);
+}
+
+static int gemv_waves(int N, int K) {
+  const int ntiles = (N + 15) / 16, ksteps = K / 32;
+  int waves = 4;
+  while (waves < 16 && ntiles * waves < 2048 && waves * 2 <= ksteps) waves *= 2;
+  return waves;
+}
+
+template <int R, int MM, bool LN>
+static void gemv_rows_launch(const bf16* X, const LnArgs& ln, const bf16* W, int M, int N, int K, const Epi& ep,
+                             hipStream_t s) {
+  const size_t shm = 256 + (LN ? (size_t)M * K * sizeof(bf16) : 0);
+  const int blocks = (N + 4 * R - 1) / (4 * R);
+  gemv_rows_kernel<R, MM, 2, LN><<<blocks, 256, shm, s>>>(W, X, ln, M, N, K, ep);
+}
+
+template <bool LN>
+static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, int M, int N, int K, const Epi& ep,
+                               hipStream_t s) {
+  if (M > 4 || (K % 8) != 0 || K < 8) return false;
+  if (ep.kind == EPI_ARGMAX) {  // a block = one 16-column tile
+    if (M == 1) gemv_rows_launch<4, 1, LN>(x, ln, w, M, N, K, ep, s);
+    else if (M == 2) gemv_rows_launch<4, 2, LN>(x, ln, w, M, N, K, ep, s);
+    else gemv_rows_launch<4, 4, LN>(x, ln, w, M, N, K, ep, s);
+    return true;
+  }
+  const bool wide = N >= 32768;  // many rows: amortise the x reads over 2 rows per wave
+  if (M == 1) { if (wide) gemv_rows_launch<2, 1, LN>(x, ln, w, M, N, K, ep, s); else gemv_rows_launch<1, 1, LN>(x, ln, w, M, N, K, ep, s); }
+  else if (M == 2) { if (wide) gemv_rows_launch<2, 2, LN>(x, ln, w, M, N, K, ep, s); else gemv_rows_launch<1, 2, LN>(x, ln, w, M, N, K, ep, s); }
+  else { if (wide) gemv_rows_launch<2, 4, LN>(x, ln, w, M, N, K, ep, s); else gemv_rows_launch<1, 4, LN>(x, ln, w, M, N, K, ep, s); }
+  return true;
+}
+
+template <bool LN>
+static void gemv_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, int M, int N, int K, const Epi& ep,
+                          hipStream_t s) {
+  if (!gemv_rows_disabled() && gemv_rows_dispatch<LN>(x, ln, w, M, N, K, ep, s)) return;
+  const int waves = gemv_waves(N, K);
+  const bool two = M > 16;
+  if (waves == 4) { if (two) gemv_launch<4, 2, LN>(x, ln, w, M, N, K, ep, s); else gemv_launch<4, 1, LN>(x, ln, w, M, N, K, ep, s); }
+  else if (waves == 8) { if (two) gemv_launch<8, 2, LN>(x, ln, w, M, N, K, ep, s); else gemv_launch<8, 1, LN>(x, ln, w, M, N, K, ep, s); }
+  else { if (two) gemv_launch<16, 2, LN>(x, ln, w, M, N, K, ep, s); else gemv_launch<16, 1, LN>(x, ln, w, M, N, K, ep, s); }
+}
+
+// LN(x) -> weight GEMM.  bf16 with M <= 8: LayerNorm fused into the GEMV prologue.  Otherwise a
+// LayerNorm kernel writes the normalised activations to `xn_scratch` first.
+void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offset, const void* gamma,
+                      const void* beta, float eps, void* xn_scratch, const void* W, int M, int N, int K,
+                      const Epi& ep, hipStream_t s) {
+  if (M <= 0) return;
+  if (is_bf16 && M <= 8 && (K % 8) == 0) {
+    LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
+    gemv_dispatch<true>(nullptr, ln, (const bf16*)W, M, N, K, ep, s);
+    return;
+  }
+  launch_layernorm(is_bf16, x, nullptr, row_stride, row_offset, gamma, beta, xn_scratch, 0, M, K, eps, s);
+  launch_linear(is_bf16, xn_scratch, W, M, N, K, ep, s);
 }
 
 void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int K, const Epi& ep, hipStream_t s) {
@@ -376,13 +755,7 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
   const bf16* x = (const bf16*)X;
   const bf16* w = (const bf16*)W;
   if (M <= 32) {
-    const int ntiles = (N + 15) / 16, ksteps = K / 32;
-    int waves = 4;
-    while (waves < 16 && ntiles * waves < 2048 && waves * 2 <= ksteps) waves *= 2;
-    const bool two = M > 16;
-    if (waves == 4) { if (two) gemv_launch<4, 2>(x, w, M, N, K, ep, s); else gemv_launch<4, 1>(x, w, M, N, K, ep, s); }
-    else if (waves == 8) { if (two) gemv_launch<8, 2>(x, w, M, N, K, ep, s); else gemv_launch<8, 1>(x, w, M, N, K, ep, s); }
-    else { if (two) gemv_launch<16, 2>(x, w, M, N, K, ep, s); else gemv_launch<16, 1>(x, w, M, N, K, ep, s); }
+    gemv_dispatch<false>(x, LnArgs{}, w, M, N, K, ep, s);
     return;
   }
   const long big = (long)((M + 127) / 128) * ((N + 127) / 128);
@@ -399,90 +772,115 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
 // Attention.  Scores = slope_h * key_pos + inv_norm * q.k (alibi.baddbmm, modeling_bloom.py
 // :270-275), causal, fp32 softmax (:283), context = P.V (:292).
 // ------------------------------------------------------------------------------------
-// Decode (S == 1): block = (chunk c, head, row b); 16 lanes per key row (8 dims each),
-// 16 keys per pass; writes the chunk's (max, sum, unnormalised context).
+// Decode (S == 1).  One 8-wave block per (row b, head).  Wave w takes the 64-position chunks
+// w, w+8, ...: 16 lanes cover one 8-dim slice each of a key/value row, so every load instruction
+// reads 4 whole rows (coalesced); the chunk's V rows are loaded together with its K rows, before
+// the softmax.  Scores = ALiBi + q.k/sqrt(hd); online softmax across the wave's chunks; the 8
+// wave partials (max, sum, context) merge through LDS.  No global atomics or fences.
 template <typename T>
-__global__ __launch_bounds__(256) void attn_decode_partial_kernel(AttnArgs a) {
-  __shared__ float sc[256];
-  __shared__ float red[16][129];
-  __shared__ float sh[4];
-  const int c = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
-  const int past = a.past_dev ? *a.past_dev : a.past;
-  const int nk = past + 1;
-  const int p0 = c * a.chunk;
-  if (p0 >= nk) return;
-  const int p1 = min(nk, p0 + a.chunk);
-  const int tid = threadIdx.x, grp = tid >> 4, dl = tid & 15;
+__global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) float qs[128];
+  __shared__ float es[8][64];
+  __shared__ float pm[8], pl[8];
+  __shared__ float pacc[8][128];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int head = blockIdx.x, b = blockIdx.y;
   const int hd = a.head_dim;
-  const bool dval = dl * 8 < hd;
-  float q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (dval) load8(a.q + (size_t)b * a.hidden + head * hd + dl * 8, q);
+  for (int d = threadIdx.x; d < hd; d += 512) qs[d] = a.q[(size_t)b * a.hidden + head * hd + d];
+  __syncthreads();
+  const int past = a.past_dev ? *a.past_dev : a.past;
+  const int nk = past + 1, nlast = nk - 1;
+  const int nch = (nk + 63) >> 6;
   const size_t rowbase = ((size_t)(a.slot + b) * a.n_head + head) * a.max_ctx;
   const T* kb = (const T*)a.k_cache + rowbase * hd;
   const T* vb = (const T*)a.v_cache + rowbase * hd;
   const float slope = a.slopes[head];
-  for (int p = p0 + grp; p < p1; p += 16) {
-    float kf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (dval) load8(kb + (size_t)p * hd + dl * 8, kf);
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; j++) s += q[j] * kf[j];
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (dl == 0) sc[p - p0] = slope * (float)p + a.inv_norm * s;
+  const int grp = lane >> 4, dl = lane & 15;
+  const bool dval = dl * 8 < hd;
+  const int doff = dval ? dl * 8 : 0;  // masked lanes re-read dims 0..7 (harmless)
+  float qv[8];
+  {
+    const float4 q0 = *reinterpret_cast<const float4*>(&qs[doff]);
+    const float4 q1 = *reinterpret_cast<const float4*>(&qs[doff + 4]);
+    qv[0] = q0.x; qv[1] = q0.y; qv[2] = q0.z; qv[3] = q0.w; qv[4] = q1.x; qv[5] = q1.y; qv[6] = q1.z; qv[7] = q1.w;
   }
-  __syncthreads();
-  const int n = p1 - p0;
-  float mx = -INFINITY;
-  for (int j = tid; j < n; j += 256) mx = fmaxf(mx, sc[j]);
-  mx = wave_max(mx);
-  if ((tid & 63) == 0) sh[tid >> 6] = mx;
-  __syncthreads();
-  mx = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
-  __syncthreads();
-  float l = 0.f;
-  for (int j = tid; j < n; j += 256) { float e = __expf(sc[j] - mx); sc[j] = e; l += e; }
-  l = block_sum_256(l, sh);
+  float m_run = -INFINITY, l_run = 0.f;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int p = p0 + grp; p < p1; p += 16) {
-    if (dval) {
-      float vf[8];
-      load8(vb + (size_t)p * hd + dl * 8, vf);
-      const float pv = sc[p - p0];
+  for (int c = w; c < nch; c += 8) {
+    typename Raw8<T>::type kr[16], vr[16];
 #pragma unroll
-      for (int j = 0; j < 8; j++) acc[j] += pv * vf[j];
+    for (int it = 0; it < 16; it++) {
+      const int pr = min(c * 64 + it * 4 + grp, nlast);
+      raw_load(kb + (size_t)pr * hd + doff, kr[it]);
     }
-  }
-  if (dval) {
 #pragma unroll
-    for (int j = 0; j < 8; j++) red[grp][dl * 8 + j] = acc[j];
+    for (int it = 0; it < 16; it++) {
+      const int pr = min(c * 64 + it * 4 + grp, nlast);
+      raw_load(vb + (size_t)pr * hd + doff, vr[it]);
+    }
+    float sc[16];
+#pragma unroll
+    for (int it = 0; it < 16; it++) {
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; j++) d += qv[j] * raw_get(kr[it], j);
+      d = dval ? d : 0.f;
+      d += __shfl_xor(d, 8, 64);
+      d += __shfl_xor(d, 4, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 1, 64);
+      sc[it] = d;
+    }
+    if (dl == 0) {
+#pragma unroll
+      for (int it = 0; it < 16; it++) es[w][it * 4 + grp] = sc[it];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int p = c * 64 + lane;
+    const bool live = p < nk;
+    const float s_me = live ? slope * (float)p + a.inv_norm * es[w][lane] : -INFINITY;
+    const float m_new = fmaxf(m_run, wave_max(s_me));
+    const float e = live ? __expf(s_me - m_new) : 0.f;
+    const float scale = __expf(m_run - m_new);  // 0 on the first chunk (m_run = -inf)
+    l_run = l_run * scale + wave_sum(e);
+#pragma unroll
+    for (int j = 0; j < 8; j++) acc[j] *= scale;
+    m_run = m_new;
+    __builtin_amdgcn_wave_barrier();
+    es[w][lane] = e;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 16; it++) {
+      const float ep = es[w][it * 4 + grp];
+#pragma unroll
+      for (int j = 0; j < 8; j++) acc[j] += ep * raw_get(vr[it], j);
+    }
+    __builtin_amdgcn_wave_barrier();
   }
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    acc[j] += __shfl_xor(acc[j], 16, 64);
+    acc[j] += __shfl_xor(acc[j], 32, 64);
+  }
+  if (grp == 0 && dval) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) pacc[w][dl * 8 + j] = acc[j];
+  }
+  if (lane == 0) { pm[w] = m_run; pl[w] = l_run; }
   __syncthreads();
-  const size_t pidx = ((size_t)b * a.n_head + head) * a.max_chunks + c;
-  if (tid < hd) {
-    float o = 0.f;
+  if (threadIdx.x < hd) {
+    float M = pm[0];
 #pragma unroll
-    for (int gg = 0; gg < 16; gg++) o += red[gg][tid];
-    a.part_acc[pidx * hd + tid] = o;
+    for (int ww = 1; ww < 8; ww++) M = fmaxf(M, pm[ww]);
+    float L = 0.f, o = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 8; ww++) {
+      const float wgt = __expf(pm[ww] - M);  // idle waves: exp(-inf) = 0
+      L += wgt * pl[ww];
+      o += wgt * pacc[ww][threadIdx.x];
+    }
+    ((T*)a.ctx_out)[(size_t)b * a.hidden + head * hd + threadIdx.x] = from_f32<T>(o / L);
   }
-  if (tid == 0) { a.part_ml[pidx * 2] = mx; a.part_ml[pidx * 2 + 1] = l; }
-}
-
-template <typename T>
-__global__ __launch_bounds__(128) void attn_decode_combine_kernel(AttnArgs a) {
-  const int head = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
-  const int past = a.past_dev ? *a.past_dev : a.past;
-  const int nch = (past + 1 + a.chunk - 1) / a.chunk;
-  const size_t base = ((size_t)b * a.n_head + head) * a.max_chunks;
-  float M = -INFINITY;
-  for (int c = 0; c < nch; c++) M = fmaxf(M, a.part_ml[(base + c) * 2]);
-  float L = 0.f, o = 0.f;
-  for (int c = 0; c < nch; c++) {
-    const float wgt = __expf(a.part_ml[(base + c) * 2] - M);
-    L += wgt * a.part_ml[(base + c) * 2 + 1];
-    if (d < a.head_dim) o += wgt * a.part_acc[(base + c) * a.head_dim + d];
-  }
-  if (d < a.head_dim) ((T*)a.ctx_out)[(size_t)b * a.hidden + head * a.head_dim + d] = from_f32<T>(o / L);
 }
 
 // S > 1: one wave per (query, head, row), online softmax over 64-key blocks.
@@ -535,7 +933,7 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(AttnArgs a) {
 }
 
 size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, int* max_chunks, int* chunk) {
-  const int ch = 64;
+  const int ch = 64;  // == the wave width of attn_decode_kernel
   const int mc = (max_ctx + ch - 1) / ch;
   *max_chunks = mc;
   *chunk = ch;
@@ -544,14 +942,9 @@ size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, 
 
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
   if (a.S == 1) {
-    dim3 g1(a.max_chunks, a.n_head, a.B), g2(a.n_head, a.B);
-    if (is_bf16) {
-      attn_decode_partial_kernel<bf16><<<g1, 256, 0, s>>>(a);
-      attn_decode_combine_kernel<bf16><<<g2, 128, 0, s>>>(a);
-    } else {
-      attn_decode_partial_kernel<float><<<g1, 256, 0, s>>>(a);
-      attn_decode_combine_kernel<float><<<g2, 128, 0, s>>>(a);
-    }
+    dim3 g(a.n_head, a.B);
+    if (is_bf16) attn_decode_kernel<bf16><<<g, 512, 0, s>>>(a);
+    else attn_decode_kernel<float><<<g, 512, 0, s>>>(a);
   } else {
     dim3 g(a.S, a.n_head, a.B);
     if (is_bf16) attn_prefill_kernel<bf16><<<g, 64, 0, s>>>(a);
@@ -560,29 +953,36 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void argmax_finalize_kernel(const unsigned long long* keys, int* tokens, int ntiles) {
-  __shared__ unsigned long long sh[4];
+__global__ __launch_bounds__(1024) void argmax_finalize_kernel(const unsigned long long* keys, int* tokens, int ntiles) {
+  __shared__ unsigned long long sh[16];
   const int m = blockIdx.x;
+  const unsigned long long* kr = keys + (size_t)m * ntiles;
   unsigned long long best = 0;
-  for (int i = threadIdx.x; i < ntiles; i += 256) {
-    unsigned long long k = keys[(size_t)m * ntiles + i];
+#pragma unroll 4
+  for (int i = threadIdx.x; i < ntiles; i += 1024) {
+    const unsigned long long k = kr[i];
     best = k > best ? k : best;
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
-    unsigned long long other = __shfl_xor(best, o, 64);
+    const unsigned long long other = __shfl_xor(best, o, 64);
     best = other > best ? other : best;
   }
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = best;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int i = 1; i < 4; i++) best = sh[i] > best ? sh[i] : best;
-    tokens[m] = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+  if (threadIdx.x < 64) {
+    best = threadIdx.x < 16 ? sh[threadIdx.x] : 0ull;
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) {
+      const unsigned long long other = __shfl_xor(best, o, 64);
+      best = other > best ? other : best;
+    }
+    if (threadIdx.x == 0) tokens[m] = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
   }
 }
 
 void launch_argmax_finalize(const unsigned long long* keys, int* tokens, int M, int ntiles, hipStream_t s) {
-  argmax_finalize_kernel<<<M, 256, 0, s>>>(keys, tokens, ntiles);
+  argmax_finalize_kernel<<<M, 1024, 0, s>>>(keys, tokens, ntiles);
 }
 
 __global__ void set_past_kernel(int* p, int v) { *p = v; }

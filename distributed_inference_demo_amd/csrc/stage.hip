@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -39,6 +40,18 @@ enum { M_WEMB = 0, M_EMB_G = 1, M_EMB_B = 2, M_LNF_G = 3, M_LNF_B = 4 };
 
 struct Layer {
   void* t[T_NLAYER];
+};
+
+struct GraphKey {
+  int B, slot, flags;
+  const void* in;
+  void* out;
+  float* logits;
+  hipStream_t st;
+  bool operator==(const GraphKey& o) const {
+    return B == o.B && slot == o.slot && flags == o.flags && in == o.in && out == o.out && logits == o.logits &&
+           st == o.st;
+  }
 };
 
 struct ProfClass {
@@ -88,6 +101,7 @@ struct bs_stage {
   int* past_dev = nullptr;
   ProfClass prof;
   std::vector<std::pair<void*, size_t>> order;  // canonical weight order (BS_WEIGHTS_HOST layout)
+  std::vector<std::pair<GraphKey, hipGraphExec_t>> graphs;  // captured decode steps
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -177,6 +191,7 @@ static void free_stage(bs_stage* s) {
   hipSetDevice(s->d.device);
   if (s->own) hipStreamSynchronize(s->own);
   for (auto e : s->prof.ev) hipEventDestroy(e);
+  for (auto& g : s->graphs) hipGraphExecDestroy(g.second);
   if (s->wbase) hipFree(s->wbase);
   if (s->kv) hipFree(s->kv);
   if (s->ws) hipFree(s->ws);
@@ -317,6 +332,7 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   s->tok = (int*)(s->ws + wo[wi++]);
   s->ids = (int*)(s->ws + wo[wi++]);
   s->past_dev = (int*)(s->ws + wo[wi++]);
+  HIP_TRY(hipMemsetAsync(s->ws, 0, s->wsbytes, s->own));
   std::vector<float> sl(desc->n_head);
   alibi_slopes(desc->n_head, sl.data());
   HIP_TRY(hipMemcpyAsync(s->slopes, sl.data(), sl.size() * 4, hipMemcpyHostToDevice, s->own));
@@ -453,21 +469,27 @@ static void linear(bs_stage* s, hipStream_t st, const void* X, const void* W, in
   }
 }
 
-extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void* out, float* logits, void* stream) {
-  if (!s || !step) return fail(BS_ERR_INVALID, "stage/step is NULL");
+static void linear_ln(bs_stage* s, hipStream_t st, const float* x, int row_stride, int row_offset, const void* g,
+                      const void* b, const void* W, int M, int N, int K, const Epi& ep, int out_bytes) {
+  const bool decode = M <= 32 && s->bf16;
+  if (decode) {
+    ProfScope p(s, st, 1, gemv_bytes(s, M, N, K, out_bytes));
+    launch_linear_ln(s->bf16, x, row_stride, row_offset, g, b, s->d.ln_eps, s->xn, W, M, N, K, ep, st);
+  } else {
+    ProfScope p(s, st, 2, 2.0 * M * N * K);
+    launch_linear_ln(s->bf16, x, row_stride, row_offset, g, b, s->d.ln_eps, s->xn, W, M, N, K, ep, st);
+  }
+}
+
+// Enqueue one forward on `st`.  With `past_dev` set, kernels read past_len from device memory
+// (graph-replayable); otherwise from the host value.
+static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, void* out, float* logits, hipStream_t st,
+                           const int* past_dev) {
   const bs_stage_desc& d = s->d;
   const int B = step->batch, S = step->seq, slot = step->slot, past = step->past_len;
   const int M = B * S;
-  if (B <= 0 || S <= 0) return fail(BS_ERR_INVALID, "batch and seq must be positive");
-  if (slot < 0 || slot + B > d.max_batch) return fail(BS_ERR_INVALID, "slot range outside max_batch");
-  if (past < 0 || past + S > d.max_ctx) return fail(BS_ERR_INVALID, "past_len + seq exceeds max_ctx");
-  if (M > d.max_tokens) return fail(BS_ERR_INVALID, "batch*seq exceeds max_tokens");
-  if (!in || !out) return fail(BS_ERR_INVALID, "in/out is NULL");
   const bool want_logits = (step->flags & BS_STEP_LOGITS) != 0;
-  if (want_logits && (!d.is_last || !logits)) return fail(BS_ERR_INVALID, "logits requested on a non-last stage or NULL");
   const bool host_io = (step->flags & BS_STEP_HOST_IO) != 0;
-  HIP_TRY(hipSetDevice(d.device));
-  hipStream_t st = stream ? (hipStream_t)stream : s->own;
   const int h = d.hidden, V = d.vocab, hd = s->hd, nh = d.n_head;
 
   // ---- input
@@ -475,8 +497,6 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
   if (d.is_first) {
     const int* ids = (const int*)in;
     if (host_io) {
-      for (int i = 0; i < M; i++)
-        if (ids[i] < 0 || ids[i] >= V) return fail(BS_ERR_INVALID, "token id out of range");
       HIP_TRY(hipMemcpyAsync(s->ids, ids, (size_t)M * 4, hipMemcpyHostToDevice, st));
       ids = s->ids;
     }
@@ -494,19 +514,17 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
   for (int l = 0; l < s->L; l++) {
     const Layer& w = s->layers[l];
     char* kbase = s->kv + l * s->kv_layer_stride;
-    // x1 = LN_in(x)
-    launch_layernorm(s->bf16, cur, nullptr, 1, 0, w.t[T_LN1_G], w.t[T_LN1_B], s->xn, 0, M, h, d.ln_eps, st);
-    // fused QKV (+bias) -> q, K/V cache
+    // x1 = LN_in(x); fused QKV (+bias) -> q, K/V cache
     Epi e{};
     e.kind = EPI_QKV; e.bias = w.t[T_QKV_B]; e.q_out = s->q; e.k_cache = kbase; e.v_cache = kbase + s->kv_half;
     e.hidden = h; e.head_dim = hd; e.max_ctx = d.max_ctx; e.n_head = nh; e.seq = S; e.slot = slot; e.past = past;
-    e.ldo = 3 * h;
-    linear(s, st, s->xn, w.t[T_QKV_W], M, 3 * h, h, e, 4);
+    e.past_dev = past_dev; e.ldo = 3 * h;
+    linear_ln(s, st, cur, 1, 0, w.t[T_LN1_G], w.t[T_LN1_B], w.t[T_QKV_W], M, 3 * h, h, e, 4);
     // attention
     AttnArgs a{};
     a.q = s->q; a.k_cache = kbase; a.v_cache = kbase + s->kv_half; a.ctx_out = s->ctx; a.slopes = s->slopes;
-    a.B = B; a.S = S; a.slot = slot; a.past = past; a.n_head = nh; a.head_dim = hd; a.max_ctx = d.max_ctx;
-    a.hidden = h; a.inv_norm = inv_norm; a.part_acc = s->part_acc; a.part_ml = s->part_ml;
+    a.B = B; a.S = S; a.slot = slot; a.past = past; a.past_dev = past_dev; a.n_head = nh; a.head_dim = hd;
+    a.max_ctx = d.max_ctx; a.hidden = h; a.inv_norm = inv_norm; a.part_acc = s->part_acc; a.part_ml = s->part_ml;
     a.max_chunks = s->max_chunks; a.chunk = s->chunk;
     {
       ProfScope p(s, st, 3, (double)B * nh * (double)(past + S) * hd * 2 * s->esz);
@@ -517,10 +535,9 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
     e2.kind = EPI_RESID; e2.bias = w.t[T_DENSE_B]; e2.out_f32 = s->attn; e2.resid = cur; e2.ldo = h;
     linear(s, st, s->ctx, w.t[T_DENSE_W], M, h, h, e2, 4);
     // x2 = LN_post(a); g = gelu(x2 W1 + b1)
-    launch_layernorm(s->bf16, s->attn, nullptr, 1, 0, w.t[T_LN2_G], w.t[T_LN2_B], s->xn, 0, M, h, d.ln_eps, st);
     Epi e3{};
     e3.kind = EPI_GELU; e3.bias = w.t[T_FC1_B]; e3.out_act = s->g; e3.ldo = 4 * h;
-    linear(s, st, s->xn, w.t[T_FC1_W], M, 4 * h, h, e3, (int)s->esz);
+    linear_ln(s, st, s->attn, 1, 0, w.t[T_LN2_G], w.t[T_LN2_B], w.t[T_FC1_W], M, 4 * h, h, e3, (int)s->esz);
     // x = a + g W2 + b2
     float* nxt = (!d.is_last && !host_io && l == s->L - 1) ? (float*)out : (cur == s->xa ? s->xb : s->xa);
     Epi e4{};
@@ -532,16 +549,14 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
   // ---- output
   if (d.is_last) {
     // ln_f on each row's last position, tied lm_head, greedy pick
-    launch_layernorm(s->bf16, cur, nullptr, S, S - 1, s->lnf_g, s->lnf_b, s->xn, 0, B, h, d.ln_eps, st);
     Epi e{};
     e.kind = EPI_ARGMAX; e.keys = s->keys; e.logits = want_logits && !host_io ? logits : nullptr; e.ldo = V;
     float* dev_logits = nullptr;
     if (want_logits && host_io) {
-      // logits go through the attention-partials-free region of the workspace? keep it simple: temp alloc
       HIP_TRY(hipMallocAsync((void**)&dev_logits, (size_t)B * V * 4, st));
       e.logits = dev_logits;
     }
-    linear(s, st, s->xn, s->wemb, B, V, h, e, 0);
+    linear_ln(s, st, cur, S, S - 1, s->lnf_g, s->lnf_b, s->wemb, B, V, h, e, 0);
     launch_argmax_finalize(s->keys, host_io ? s->tok : (int*)out, B, V / 16, st);
     if (host_io) {
       HIP_TRY(hipMemcpyAsync(out, s->tok, (size_t)B * 4, hipMemcpyDeviceToHost, st));
@@ -554,6 +569,69 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
     HIP_TRY(hipMemcpyAsync(out, cur, (size_t)M * h * 4, hipMemcpyDeviceToHost, st));
   } else if (s->L == 0) {
     HIP_TRY(hipMemcpyAsync(out, cur, (size_t)M * h * 4, hipMemcpyDeviceToDevice, st));
+  }
+  return BS_OK;
+}
+
+static bool graphs_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("BS_NO_GRAPH");
+    on = !(e && *e && *e != '0');
+  }
+  return on != 0;
+}
+
+extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void* out, float* logits, void* stream) {
+  if (!s || !step) return fail(BS_ERR_INVALID, "stage/step is NULL");
+  const bs_stage_desc& d = s->d;
+  const int B = step->batch, S = step->seq, slot = step->slot, past = step->past_len;
+  const int M = B * S;
+  if (B <= 0 || S <= 0) return fail(BS_ERR_INVALID, "batch and seq must be positive");
+  if (slot < 0 || slot + B > d.max_batch) return fail(BS_ERR_INVALID, "slot range outside max_batch");
+  if (past < 0 || past + S > d.max_ctx) return fail(BS_ERR_INVALID, "past_len + seq exceeds max_ctx");
+  if (M > d.max_tokens) return fail(BS_ERR_INVALID, "batch*seq exceeds max_tokens");
+  if (!in || !out) return fail(BS_ERR_INVALID, "in/out is NULL");
+  const bool want_logits = (step->flags & BS_STEP_LOGITS) != 0;
+  if (want_logits && (!d.is_last || !logits)) return fail(BS_ERR_INVALID, "logits requested on a non-last stage or NULL");
+  const bool host_io = (step->flags & BS_STEP_HOST_IO) != 0;
+  if (d.is_first && host_io) {
+    const int* ids = (const int*)in;
+    for (int i = 0; i < M; i++)
+      if (ids[i] < 0 || ids[i] >= d.vocab) return fail(BS_ERR_INVALID, "token id out of range");
+  }
+  HIP_TRY(hipSetDevice(d.device));
+  hipStream_t st = stream ? (hipStream_t)stream : s->own;
+
+  // Decode steps on device buffers replay a captured hipGraph: the kernels read past_len from
+  // device memory, set by one small kernel ahead of the replay.
+  const bool graph = S == 1 && !host_io && s->prof.cls == 0 && graphs_enabled();
+  if (graph) {
+    GraphKey key{B, slot, step->flags, in, out, logits, st};
+    hipGraphExec_t exec = nullptr;
+    for (auto& g : s->graphs)
+      if (g.first == key) { exec = g.second; break; }
+    if (!exec) {
+      hipGraph_t gr = nullptr;
+      HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+      int rc = enqueue_forward(s, step, in, out, logits, st, s->past_dev);
+      hipError_t ce = hipStreamEndCapture(st, &gr);
+      if (rc != BS_OK) { if (gr) hipGraphDestroy(gr); return rc; }
+      if (ce != hipSuccess) return fail(BS_ERR_DEVICE, std::string("graph capture: ") + hipGetErrorString(ce));
+      hipError_t ie = hipGraphInstantiate(&exec, gr, nullptr, nullptr, 0);
+      hipGraphDestroy(gr);
+      if (ie != hipSuccess) return fail(BS_ERR_DEVICE, std::string("graph instantiate: ") + hipGetErrorString(ie));
+      if (s->graphs.size() >= 64) {
+        hipGraphExecDestroy(s->graphs.front().second);
+        s->graphs.erase(s->graphs.begin());
+      }
+      s->graphs.push_back({key, exec});
+    }
+    launch_set_past(s->past_dev, past, st);
+    HIP_TRY(hipGraphLaunch(exec, st));
+  } else {
+    int rc = enqueue_forward(s, step, in, out, logits, st, nullptr);
+    if (rc != BS_OK) return rc;
   }
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(BS_ERR_DEVICE, std::string("kernel launch: ") + hipGetErrorString(err));

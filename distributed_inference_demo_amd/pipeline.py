@@ -175,6 +175,8 @@ def bench_pipeline(args):
     B, P, K, W = args.batch, args.prompt, args.steps, args.warmup
     pipe, (lb, le) = build_rank(model, rank, world, dev, dtype=args.dtype, mb_rows=B, n_mb=world,
                                 max_ctx=P + W + K + 2, max_seq=P, seed=args.seed)
+    cs = torch.cuda.Stream()  # a real stream: decode steps are captured as hipGraphs
+    torch.cuda.set_stream(cs)
     prompt = None
     if rank == 0:
         from .stage import prompt_ids

@@ -1,0 +1,13 @@
+# GPU check: parity tests, bench, then a rocprofv3 kernel-trace of the default bench workload.
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1
+rc=$?
+echo "bench rc=$rc" >> gpurun_out/bench.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python -u bench.py --cpu-baseline 0 > gpurun_out/prof_bench.log 2>&1
+echo "prof rc=$?" >> gpurun_out/prof_bench.log
