@@ -29,10 +29,12 @@ struct Epi {
   // EPI_ARGMAX
   unsigned long long* keys;  // [M][N/16]: max over each 16-column tile
   float* logits;          // optional [M][ldo]
+  int col_offset;         // vocabulary index of column 0 (head slices)
 };
 
 // dtype tag: 0 = fp32, 1 = bf16
-void launch_gen_fill(void* dst, int is_bf16, uint64_t n, uint64_t key, int kind, hipStream_t s);
+void launch_gen_fill(void* dst, int is_bf16, uint64_t n, uint64_t key, int kind, hipStream_t s,
+                     uint64_t index_offset = 0);
 void launch_convert_f32(void* dst, int is_bf16, const float* src, uint64_t n, hipStream_t s);
 
 // LayerNorm rows: out[m] (T, or fp32 when out_f32) = LN(x[m*row_stride + row_offset]) with
@@ -72,5 +74,7 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s);
 size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, int* max_chunks, int* chunk);
 
 // keys -> token ids
-void launch_argmax_finalize(const unsigned long long* keys, int* tokens, int M, int ntiles, hipStream_t s);
+// Reduce the per-tile keys of each row (and keys_in[m] if given) -> keys_out[m] / tokens[m] (either optional).
+void launch_argmax_finalize(const unsigned long long* keys, int M, int ntiles, const unsigned long long* keys_in,
+                            unsigned long long* keys_out, int* tokens, hipStream_t s);
 void launch_set_past(int* past_dev, int value, hipStream_t s);

@@ -47,9 +47,9 @@ __device__ __forceinline__ float d_gen_value(int kind, uint64_t key, uint64_t ke
 }
 
 template <typename T>
-__global__ void gen_fill_kernel(T* dst, uint64_t n, uint64_t key, uint64_t key2, int kind) {
+__global__ void gen_fill_kernel(T* dst, uint64_t n, uint64_t key, uint64_t key2, int kind, uint64_t off) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    dst[i] = from_f32<T>(d_gen_value(kind, key, key2, (uint32_t)i));
+    dst[i] = from_f32<T>(d_gen_value(kind, key, key2, (uint32_t)(i + off)));
 }
 
 template <typename T>
@@ -65,14 +65,14 @@ static uint64_t h_sm64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-void launch_gen_fill(void* dst, int is_bf16, uint64_t n, uint64_t key, int kind, hipStream_t s) {
+void launch_gen_fill(void* dst, int is_bf16, uint64_t n, uint64_t key, int kind, hipStream_t s, uint64_t off) {
   uint64_t blocks = (n + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks == 0) return;
   if (is_bf16)
-    gen_fill_kernel<bf16><<<(unsigned)blocks, 256, 0, s>>>((bf16*)dst, n, key, h_sm64(key), kind);
+    gen_fill_kernel<bf16><<<(unsigned)blocks, 256, 0, s>>>((bf16*)dst, n, key, h_sm64(key), kind, off);
   else
-    gen_fill_kernel<float><<<(unsigned)blocks, 256, 0, s>>>((float*)dst, n, key, h_sm64(key), kind);
+    gen_fill_kernel<float><<<(unsigned)blocks, 256, 0, s>>>((float*)dst, n, key, h_sm64(key), kind, off);
 }
 
 void launch_convert_f32(void* dst, int is_bf16, const float* src, uint64_t n, hipStream_t s) {
@@ -143,7 +143,8 @@ void launch_layernorm(int is_bf16, const void* x, const int* ids, int row_stride
 // 16 consecutive lanes (same lane>>4) hold the 16 columns of one output row: reduce the
 // (value, column) argmax over them and let the column-0 lane store the tile's key.
 __device__ __forceinline__ void argmax_tile16(const Epi& e, int m, int n, float v, bool valid, int ntiles) {
-  unsigned long long key = valid ? (((unsigned long long)f32_order_key(v) << 32) | (0xFFFFFFFFu - (uint32_t)n)) : 0ull;
+  unsigned long long key =
+      valid ? (((unsigned long long)f32_order_key(v) << 32) | (0xFFFFFFFFu - (uint32_t)(n + e.col_offset))) : 0ull;
 #pragma unroll
   for (int o = 8; o >= 1; o >>= 1) {
     unsigned long long other = __shfl_xor(key, o, 64);
@@ -398,70 +399,79 @@ __device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float ac
   return acc;
 }
 
-// LayerNorm of M <= 8 rows into LDS (bf16), 256 threads.  nn.LayerNorm semantics.
+// LayerNorm of M <= MM <= 4 rows (K <= 4096) into LDS as bf16, 256 threads, nn.LayerNorm
+// semantics.  Each thread keeps its <= 16 values per row in registers: one global pass, two
+// block reductions (mean, then the exact centred variance), normalise from registers.
+template <int MM>
 __device__ __forceinline__ void ln_rows_to_lds(const LnArgs& ln, int M, int K, bf16* xs, float* scratch) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float* st = scratch;           // [0..7] mean, [8..15] rstd
-  float* wp_part = scratch + 16; // [4 waves][8]
-  float part[8];
+  float4 xv[MM][4];
+  float part[MM];
 #pragma unroll
-  for (int m = 0; m < 8; m++) {
-    part[m] = 0.f;
-    if (m < M) {
-      const float* xr = ln.x + ((size_t)m * ln.row_stride + ln.row_offset) * K;
-      float acc = 0.f;
-      for (int k = threadIdx.x * 4; k < K; k += 1024) {
-        const float4 v = *reinterpret_cast<const float4*>(xr + k);
-        acc += (v.x + v.y) + (v.z + v.w);
-      }
-      part[m] = wave_sum(acc);
+  for (int m = 0; m < MM; m++) {
+    const float* xr = ln.x + ((size_t)min(m, M - 1) * ln.row_stride + ln.row_offset) * K;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int k = threadIdx.x * 4 + i * 1024;
+      xv[m][i] = k < K ? *reinterpret_cast<const float4*>(xr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      acc += (xv[m][i].x + xv[m][i].y) + (xv[m][i].z + xv[m][i].w);
     }
+    part[m] = wave_sum(acc);
   }
   if (lane == 0) {
 #pragma unroll
-    for (int m = 0; m < 8; m++) if (m < M) wp_part[w * 8 + m] = part[m];
+    for (int m = 0; m < MM; m++) scratch[16 + w * 8 + m] = part[m];
   }
   __syncthreads();
-  if (threadIdx.x < M) st[threadIdx.x] = (wp_part[threadIdx.x] + wp_part[8 + threadIdx.x] + wp_part[16 + threadIdx.x] +
-                                          wp_part[24 + threadIdx.x]) / (float)K;
-  __syncthreads();
+  float mean[MM], rstd[MM];
 #pragma unroll
-  for (int m = 0; m < 8; m++) {
-    if (m < M) {
-      const float* xr = ln.x + ((size_t)m * ln.row_stride + ln.row_offset) * K;
-      const float mean = st[m];
-      float acc = 0.f;
-      for (int k = threadIdx.x * 4; k < K; k += 1024) {
-        const float4 v = *reinterpret_cast<const float4*>(xr + k);
-        const float d0 = v.x - mean, d1 = v.y - mean, d2 = v.z - mean, d3 = v.w - mean;
+  for (int m = 0; m < MM; m++)
+    mean[m] = (scratch[16 + m] + scratch[24 + m] + scratch[32 + m] + scratch[40 + m]) / (float)K;
+#pragma unroll
+  for (int m = 0; m < MM; m++) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int k = threadIdx.x * 4 + i * 1024;
+      if (k < K) {
+        const float d0 = xv[m][i].x - mean[m], d1 = xv[m][i].y - mean[m], d2 = xv[m][i].z - mean[m],
+                    d3 = xv[m][i].w - mean[m];
         acc += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
       }
-      part[m] = wave_sum(acc);
     }
+    part[m] = wave_sum(acc);
   }
   __syncthreads();
   if (lane == 0) {
 #pragma unroll
-    for (int m = 0; m < 8; m++) if (m < M) wp_part[w * 8 + m] = part[m];
+    for (int m = 0; m < MM; m++) scratch[16 + w * 8 + m] = part[m];
   }
   __syncthreads();
-  if (threadIdx.x < M) {
-    const float t = wp_part[threadIdx.x] + wp_part[8 + threadIdx.x] + wp_part[16 + threadIdx.x] + wp_part[24 + threadIdx.x];
-    st[8 + threadIdx.x] = 1.0f / sqrtf(t / (float)K + ln.eps);
-  }
-  __syncthreads();
-  for (int m = 0; m < M; m++) {
-    const float* xr = ln.x + ((size_t)m * ln.row_stride + ln.row_offset) * K;
-    const float mean = st[m], rstd = st[8 + m];
-    for (int k = threadIdx.x * 8; k < K; k += 2048) {
-      float xv[8], gv[8], bv[8];
-      load8(xr + k, xv);
-      load8(ln.gamma + k, gv);
-      load8(ln.beta + k, bv);
-      bf16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; j++) o[j] = (bf16)((xv[j] - mean) * rstd * gv[j] + bv[j]);
-      *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + k) = o;
+  for (int m = 0; m < MM; m++)
+    rstd[m] = 1.0f / sqrtf((scratch[16 + m] + scratch[24 + m] + scratch[32 + m] + scratch[40 + m]) / (float)K + ln.eps);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int k = threadIdx.x * 4 + i * 1024;
+    if (k < K) {
+      const uint2 graw = *reinterpret_cast<const uint2*>(ln.gamma + k);
+      const uint2 braw = *reinterpret_cast<const uint2*>(ln.beta + k);
+      const float g[4] = {__uint_as_float(graw.x << 16), __uint_as_float(graw.x & 0xFFFF0000u),
+                          __uint_as_float(graw.y << 16), __uint_as_float(graw.y & 0xFFFF0000u)};
+      const float bb[4] = {__uint_as_float(braw.x << 16), __uint_as_float(braw.x & 0xFFFF0000u),
+                           __uint_as_float(braw.y << 16), __uint_as_float(braw.y & 0xFFFF0000u)};
+#pragma unroll
+      for (int m = 0; m < MM; m++) {
+        if (m < M) {
+          const float v[4] = {xv[m][i].x, xv[m][i].y, xv[m][i].z, xv[m][i].w};
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; j++) o[j] = (bf16)((v[j] - mean[m]) * rstd[m] * g[j] + bb[j]);
+          *reinterpret_cast<bf16x4*>(xs + (size_t)m * K + k) = o;
+        }
+      }
     }
   }
   __syncthreads();
@@ -478,10 +488,19 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
   const bf16* wr[R];
 #pragma unroll
   for (int r = 0; r < R; r++) wr[r] = W + (size_t)min(n0 + r, N - 1) * K;
+  // the first U chunks of every row are requested before the (LN) prologue, so the weight
+  // stream is already in flight while the block normalises its activations
+  bf16x8 wv[U][R];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int k = min(u * 512 + lane * 8, K - 8);
+#pragma unroll
+    for (int r = 0; r < R; r++) wv[u][r] = *reinterpret_cast<const bf16x8*>(wr[r] + k);
+  }
   const bf16* xg;
   int xstride;
   if constexpr (LN) {
-    ln_rows_to_lds(ln, M, K, xs, scratch);
+    ln_rows_to_lds<MM>(ln, M, K, xs, scratch);
     xg = xs; xstride = K;
   } else {
     xg = X; xstride = K;
@@ -493,12 +512,13 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
     for (int m = 0; m < MM; m++) acc[r][m] = 0.f;
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   for (int kb = 0; kb < K; kb += 512 * U) {
-    bf16x8 wv[U][R];
+    if (kb) {
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int k = min(kb + u * 512 + lane * 8, K - 8);
+      for (int u = 0; u < U; u++) {
+        const int k = min(kb + u * 512 + lane * 8, K - 8);
 #pragma unroll
-      for (int r = 0; r < R; r++) wv[u][r] = *reinterpret_cast<const bf16x8*>(wr[r] + k);
+        for (int r = 0; r < R; r++) wv[u][r] = *reinterpret_cast<const bf16x8*>(wr[r] + k);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -705,14 +725,17 @@ static void gemv_rows_launch(const bf16* X, const LnArgs& ln, const bf16* W, int
 template <bool LN>
 static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, int M, int N, int K, const Epi& ep,
                                hipStream_t s) {
-  if (M > 4 || (K % 8) != 0 || K < 8) return false;
+  if (M > 4 || (K % 8) != 0 || K < 8 || (LN && K > 4096)) return false;
+  // M = 3..4: rows loses to the MFMA GEMV on LN-fused and large shapes
+  // (tools/gemv_bench.hip, profiles/r01_gemv_bench_m4.log); keep it for small plain GEMVs and the head.
+  if (M > 2 && ep.kind != EPI_ARGMAX && (LN || (size_t)N * K > (size_t)16 << 20)) return false;
   if (ep.kind == EPI_ARGMAX) {  // a block = one 16-column tile
     if (M == 1) gemv_rows_launch<4, 1, LN>(x, ln, w, M, N, K, ep, s);
     else if (M == 2) gemv_rows_launch<4, 2, LN>(x, ln, w, M, N, K, ep, s);
     else gemv_rows_launch<4, 4, LN>(x, ln, w, M, N, K, ep, s);
     return true;
   }
-  const bool wide = N >= 32768;  // many rows: amortise the x reads over 2 rows per wave
+  const bool wide = N >= 8192;  // many rows: 2 rows per wave amortise the x reads and the LN prologue
   if (M == 1) { if (wide) gemv_rows_launch<2, 1, LN>(x, ln, w, M, N, K, ep, s); else gemv_rows_launch<1, 1, LN>(x, ln, w, M, N, K, ep, s); }
   else if (M == 2) { if (wide) gemv_rows_launch<2, 2, LN>(x, ln, w, M, N, K, ep, s); else gemv_rows_launch<1, 2, LN>(x, ln, w, M, N, K, ep, s); }
   else { if (wide) gemv_rows_launch<2, 4, LN>(x, ln, w, M, N, K, ep, s); else gemv_rows_launch<1, 4, LN>(x, ln, w, M, N, K, ep, s); }
@@ -772,21 +795,23 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
 // Attention.  Scores = slope_h * key_pos + inv_norm * q.k (alibi.baddbmm, modeling_bloom.py
 // :270-275), causal, fp32 softmax (:283), context = P.V (:292).
 // ------------------------------------------------------------------------------------
-// Decode (S == 1).  One 8-wave block per (row b, head).  Wave w takes the 64-position chunks
-// w, w+8, ...: 16 lanes cover one 8-dim slice each of a key/value row, so every load instruction
-// reads 4 whole rows (coalesced); the chunk's V rows are loaded together with its K rows, before
-// the softmax.  Scores = ALiBi + q.k/sqrt(hd); online softmax across the wave's chunks; the 8
-// wave partials (max, sum, context) merge through LDS.  No global atomics or fences.
-template <typename T>
-__global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
+// Decode (S == 1).  Block (head, row b, split) of WV waves; wave w of split sp takes the 64-position
+// chunks c = w + WV*(sp + nsplit*j).  16 lanes cover one 8-dim slice each of a key/value row, so
+// every load instruction reads 4 whole rows (coalesced); a chunk's V rows are loaded together with
+// its K rows, before the softmax.  Scores = ALiBi + q.k/sqrt(hd); online softmax across the wave's
+// chunks; the wave partials merge through LDS.  nsplit == 1: the block writes ctx; otherwise it
+// writes a (max, sum, context) partial that attn_merge_kernel combines (small B*heads: spreads the
+// KV stream of one (row, head) over several CUs).  No global atomics or fences.
+template <typename T, int WV>
+__global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float qs[128];
-  __shared__ float es[8][64];
-  __shared__ float pm[8], pl[8];
-  __shared__ float pacc[8][128];
+  __shared__ float es[WV][64];
+  __shared__ float pm[WV], pl[WV];
+  __shared__ float pacc[WV][128];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int head = blockIdx.x, b = blockIdx.y;
+  const int head = blockIdx.x, b = blockIdx.y, sp = blockIdx.z, nsplit = gridDim.z;
   const int hd = a.head_dim;
-  for (int d = threadIdx.x; d < hd; d += 512) qs[d] = a.q[(size_t)b * a.hidden + head * hd + d];
+  for (int d = threadIdx.x; d < hd; d += WV * 64) qs[d] = a.q[(size_t)b * a.hidden + head * hd + d];
   __syncthreads();
   const int past = a.past_dev ? *a.past_dev : a.past;
   const int nk = past + 1, nlast = nk - 1;
@@ -806,7 +831,7 @@ __global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
   }
   float m_run = -INFINITY, l_run = 0.f;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int c = w; c < nch; c += 8) {
+  for (int c = w + WV * sp; c < nch; c += WV * nsplit) {
     typename Raw8<T>::type kr[16], vr[16];
 #pragma unroll
     for (int it = 0; it < 16; it++) {
@@ -871,16 +896,42 @@ __global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
   if (threadIdx.x < hd) {
     float M = pm[0];
 #pragma unroll
-    for (int ww = 1; ww < 8; ww++) M = fmaxf(M, pm[ww]);
+    for (int ww = 1; ww < WV; ww++) M = fmaxf(M, pm[ww]);
     float L = 0.f, o = 0.f;
+    if (M != -INFINITY) {  // a split past the context end holds no chunk
 #pragma unroll
-    for (int ww = 0; ww < 8; ww++) {
-      const float wgt = __expf(pm[ww] - M);  // idle waves: exp(-inf) = 0
-      L += wgt * pl[ww];
-      o += wgt * pacc[ww][threadIdx.x];
+      for (int ww = 0; ww < WV; ww++) {
+        const float wgt = __expf(pm[ww] - M);  // idle waves: exp(-inf) = 0
+        L += wgt * pl[ww];
+        o += wgt * pacc[ww][threadIdx.x];
+      }
     }
-    ((T*)a.ctx_out)[(size_t)b * a.hidden + head * hd + threadIdx.x] = from_f32<T>(o / L);
+    if (nsplit == 1) {
+      ((T*)a.ctx_out)[(size_t)b * a.hidden + head * hd + threadIdx.x] = from_f32<T>(o / L);
+    } else {
+      const size_t pidx = ((size_t)b * a.n_head + head) * a.max_chunks + sp;
+      a.part_acc[pidx * hd + threadIdx.x] = o;
+      if (threadIdx.x == 0) { a.part_ml[pidx * 2] = M; a.part_ml[pidx * 2 + 1] = L; }
+    }
   }
+}
+
+// Merge the nsplit partials of each (row, head) into ctx.
+template <typename T>
+__global__ __launch_bounds__(128) void attn_merge_kernel(AttnArgs a, int nsplit) {
+  const int head = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+  const size_t base = ((size_t)b * a.n_head + head) * a.max_chunks;
+  float M = -INFINITY;
+  for (int sp = 0; sp < nsplit; sp++) M = fmaxf(M, a.part_ml[(base + sp) * 2]);
+  float L = 0.f, o = 0.f;
+  for (int sp = 0; sp < nsplit; sp++) {
+    const float m = a.part_ml[(base + sp) * 2];
+    if (m == -INFINITY) continue;
+    const float wgt = __expf(m - M);
+    L += wgt * a.part_ml[(base + sp) * 2 + 1];
+    if (d < a.head_dim) o += wgt * a.part_acc[(base + sp) * a.head_dim + d];
+  }
+  if (d < a.head_dim) ((T*)a.ctx_out)[(size_t)b * a.hidden + head * a.head_dim + d] = from_f32<T>(o / L);
 }
 
 // S > 1: one wave per (query, head, row), online softmax over 64-key blocks.
@@ -942,9 +993,29 @@ size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, 
 
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
   if (a.S == 1) {
-    dim3 g(a.n_head, a.B);
-    if (is_bf16) attn_decode_kernel<bf16><<<g, 512, 0, s>>>(a);
-    else attn_decode_kernel<float><<<g, 512, 0, s>>>(a);
+    // One 8-wave block per (row, head) when that already fills the chip; otherwise 4-wave
+    // blocks split the context so ~256 blocks stream the KV cache, then a merge kernel.
+    // Measured (bloom-1b1, B = 1, ctx ~600): one block per (row, head) 9.2 us vs split + merge
+    // 6.6 + 4.6 us — a kernel costs ~4 us of fixed latency at this size, so split only when a
+    // single block would walk more than 2 chunks per wave (ctx > 1024).
+    const int pairs = a.B * a.n_head;
+    if (pairs >= 192 || a.max_chunks <= 16) {
+      dim3 g(a.n_head, a.B, 1);
+      if (is_bf16) attn_decode_kernel<bf16, 8><<<g, 512, 0, s>>>(a);
+      else attn_decode_kernel<float, 8><<<g, 512, 0, s>>>(a);
+    } else {
+      int nsplit = (256 + pairs - 1) / pairs;
+      nsplit = min(nsplit, (a.max_chunks + 3) / 4);
+      nsplit = max(nsplit, 1);
+      dim3 g(a.n_head, a.B, nsplit), gm(a.n_head, a.B);
+      if (is_bf16) {
+        attn_decode_kernel<bf16, 4><<<g, 256, 0, s>>>(a);
+        if (nsplit > 1) attn_merge_kernel<bf16><<<gm, 128, 0, s>>>(a, nsplit);
+      } else {
+        attn_decode_kernel<float, 4><<<g, 256, 0, s>>>(a);
+        if (nsplit > 1) attn_merge_kernel<float><<<gm, 128, 0, s>>>(a, nsplit);
+      }
+    }
   } else {
     dim3 g(a.S, a.n_head, a.B);
     if (is_bf16) attn_prefill_kernel<bf16><<<g, 64, 0, s>>>(a);
@@ -953,7 +1024,9 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void argmax_finalize_kernel(const unsigned long long* keys, int* tokens, int ntiles) {
+__global__ __launch_bounds__(1024) void argmax_finalize_kernel(const unsigned long long* keys, int ntiles,
+                                                                const unsigned long long* keys_in,
+                                                                unsigned long long* keys_out, int* tokens) {
   __shared__ unsigned long long sh[16];
   const int m = blockIdx.x;
   const unsigned long long* kr = keys + (size_t)m * ntiles;
@@ -977,12 +1050,17 @@ __global__ __launch_bounds__(1024) void argmax_finalize_kernel(const unsigned lo
       const unsigned long long other = __shfl_xor(best, o, 64);
       best = other > best ? other : best;
     }
-    if (threadIdx.x == 0) tokens[m] = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+    if (threadIdx.x == 0) {
+      if (keys_in) best = keys_in[m] > best ? keys_in[m] : best;
+      if (keys_out) keys_out[m] = best;
+      if (tokens) tokens[m] = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+    }
   }
 }
 
-void launch_argmax_finalize(const unsigned long long* keys, int* tokens, int M, int ntiles, hipStream_t s) {
-  argmax_finalize_kernel<<<M, 1024, 0, s>>>(keys, tokens, ntiles);
+void launch_argmax_finalize(const unsigned long long* keys, int M, int ntiles, const unsigned long long* keys_in,
+                            unsigned long long* keys_out, int* tokens, hipStream_t s) {
+  argmax_finalize_kernel<<<M, 1024, 0, s>>>(keys, ntiles, keys_in, keys_out, tokens);
 }
 
 __global__ void set_past_kernel(int* p, int v) { *p = v; }

@@ -77,6 +77,8 @@ struct bs_stage {
   void* emb_b = nullptr;
   void* lnf_g = nullptr;
   void* lnf_b = nullptr;
+  void* hw = nullptr;     // head slice rows [hv0, hv1) of the tied lm_head (may point into wemb)
+  int hv0 = 0, hv1 = 0;
   std::vector<Layer> layers;
   char* kv = nullptr;  // [L][2][max_batch][heads][max_ctx][hd]
   size_t kvbytes = 0;
@@ -154,6 +156,9 @@ static int validate(const bs_stage_desc* d) {
   if (d->dtype != BS_DT_BFLOAT16 && d->dtype != BS_DT_FLOAT) return fail(BS_ERR_INVALID, "dtype must be BFLOAT16 or FLOAT");
   if (d->max_batch <= 0 || d->max_ctx <= 0) return fail(BS_ERR_INVALID, "max_batch/max_ctx must be positive");
   if (!(d->ln_eps > 0.f)) return fail(BS_ERR_INVALID, "ln_eps must be positive");
+  if (d->head_vocab_begin < 0 || d->head_vocab_end < d->head_vocab_begin || d->head_vocab_end > d->vocab ||
+      d->head_vocab_begin % 16 || d->head_vocab_end % 16)
+    return fail(BS_ERR_INVALID, "head vocab slice must be a 16-aligned sub-range of [0, vocab)");
   if (d->weight_source != BS_WEIGHTS_SYNTHETIC && d->weight_source != BS_WEIGHTS_HOST)
     return fail(BS_ERR_INVALID, "unknown weight_source");
   return BS_OK;
@@ -167,6 +172,9 @@ extern "C" uint64_t bs_stage_weight_count(const bs_stage_desc* d) {
   if (d->is_first) n += 2 * h;
   n += (uint64_t)(d->layer_end - d->layer_begin) * (12 * h * h + 13 * h);
   if (d->is_last) n += 2 * h;
+  const bool slice = d->head_vocab_end > d->head_vocab_begin;
+  if (slice && !d->is_first && !d->is_last) n += (uint64_t)(d->head_vocab_end - d->head_vocab_begin) * h;
+  if (slice && !d->is_last) n += 2 * h;
   return n;
 }
 
@@ -234,6 +242,12 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   for (int l = 0; l < s->L; l++)
     for (int t = 0; t < T_NLAYER; t++) add(lsz[t]);
   if (desc->is_last) { add(h); add(h); }
+  const bool slice = desc->head_vocab_end > desc->head_vocab_begin;
+  s->hv0 = desc->head_vocab_begin;
+  s->hv1 = desc->head_vocab_end;
+  const size_t hrows = (size_t)(s->hv1 - s->hv0);
+  if (slice && !desc->is_first && !desc->is_last) add(hrows * h);
+  if (slice && !desc->is_last) { add(h); add(h); }
   s->wbytes = off;
   if (hipMalloc(&s->wbase, s->wbytes ? s->wbytes : 256) != hipSuccess)
     return cleanup(fail(BS_ERR_OOM, "weight allocation failed (" + std::to_string(s->wbytes) + " B)"));
@@ -244,11 +258,20 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   for (int l = 0; l < s->L; l++)
     for (int t = 0; t < T_NLAYER; t++) s->layers[l].t[t] = s->wbase + offs[oi++];
   if (desc->is_last) { s->lnf_g = s->wbase + offs[oi++]; s->lnf_b = s->wbase + offs[oi++]; }
+  if (slice) {
+    if (s->wemb) s->hw = (char*)s->wemb + (size_t)s->hv0 * h * s->esz;
+    else s->hw = s->wbase + offs[oi++];
+    if (!desc->is_last) { s->lnf_g = s->wbase + offs[oi++]; s->lnf_b = s->wbase + offs[oi++]; }
+  } else if (desc->is_last) {
+    s->hw = s->wemb; s->hv0 = 0; s->hv1 = desc->vocab;  // the last stage's full head
+  }
   if (s->wemb) s->order.push_back({s->wemb, V * h});
   if (s->emb_g) { s->order.push_back({s->emb_g, h}); s->order.push_back({s->emb_b, h}); }
   for (int l = 0; l < s->L; l++)
     for (int t = 0; t < T_NLAYER; t++) s->order.push_back({s->layers[l].t[t], lsz[t]});
-  if (s->lnf_g) { s->order.push_back({s->lnf_g, h}); s->order.push_back({s->lnf_b, h}); }
+  if (desc->is_last) { s->order.push_back({s->lnf_g, h}); s->order.push_back({s->lnf_b, h}); }
+  if (slice && !desc->is_first && !desc->is_last) s->order.push_back({s->hw, hrows * h});
+  if (slice && !desc->is_last) { s->order.push_back({s->lnf_g, h}); s->order.push_back({s->lnf_b, h}); }
 
   // ---- weights
   if (desc->weight_source == BS_WEIGHTS_SYNTHETIC) {
@@ -260,6 +283,8 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
       for (int t = 0; t < T_NLAYER; t++)
         launch_gen_fill(s->layers[l].t[t], s->bf16, lsz[t], tensor_key(seed, desc->layer_begin + l, t), layer_kind(t),
                         s->own);
+    if (slice && !s->wemb)
+      launch_gen_fill(s->hw, s->bf16, hrows * h, tensor_key(seed, -1, M_WEMB), 0, s->own, (uint64_t)s->hv0 * h);
     if (s->lnf_g) launch_gen_fill(s->lnf_g, s->bf16, h, tensor_key(seed, -1, M_LNF_G), 2, s->own);
     if (s->lnf_b) launch_gen_fill(s->lnf_b, s->bf16, h, tensor_key(seed, -1, M_LNF_B), 3, s->own);
   } else {
@@ -557,7 +582,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
       e.logits = dev_logits;
     }
     linear_ln(s, st, cur, S, S - 1, s->lnf_g, s->lnf_b, s->wemb, B, V, h, e, 0);
-    launch_argmax_finalize(s->keys, host_io ? s->tok : (int*)out, B, V / 16, st);
+    launch_argmax_finalize(s->keys, B, V / 16, nullptr, nullptr, host_io ? s->tok : (int*)out, st);
     if (host_io) {
       HIP_TRY(hipMemcpyAsync(out, s->tok, (size_t)B * 4, hipMemcpyDeviceToHost, st));
       if (dev_logits) {
@@ -570,6 +595,36 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
   } else if (s->L == 0) {
     HIP_TRY(hipMemcpyAsync(out, cur, (size_t)M * h * 4, hipMemcpyDeviceToDevice, st));
   }
+  return BS_OK;
+}
+
+extern "C" int bs_head_norm(bs_stage* s, const float* hidden, int32_t B, int32_t S, void* xn, void* stream) {
+  if (!s || !hidden || !xn) return fail(BS_ERR_INVALID, "stage/hidden/xn is NULL");
+  if (!s->lnf_g) return fail(BS_ERR_STATE, "stage has no ln_f (needs is_last or a head slice)");
+  if (B <= 0 || S <= 0 || B > s->d.max_batch) return fail(BS_ERR_INVALID, "bad batch/seq");
+  HIP_TRY(hipSetDevice(s->d.device));
+  hipStream_t st = stream ? (hipStream_t)stream : s->own;
+  launch_layernorm(s->bf16, hidden, nullptr, S, S - 1, s->lnf_g, s->lnf_b, xn, 0, B, s->d.hidden, s->d.ln_eps, st);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return fail(BS_ERR_DEVICE, std::string("head_norm: ") + hipGetErrorString(err));
+  return BS_OK;
+}
+
+extern "C" int bs_head_slice(bs_stage* s, const void* xn, int32_t B, const uint64_t* keys_in, uint64_t* keys_out,
+                             int32_t* tokens, void* stream) {
+  if (!s || !xn) return fail(BS_ERR_INVALID, "stage/xn is NULL");
+  if (!s->hw || s->hv1 <= s->hv0) return fail(BS_ERR_STATE, "stage has no head slice");
+  if (B <= 0 || B > s->d.max_batch) return fail(BS_ERR_INVALID, "bad batch");
+  HIP_TRY(hipSetDevice(s->d.device));
+  hipStream_t st = stream ? (hipStream_t)stream : s->own;
+  const int n = s->hv1 - s->hv0;
+  Epi e{};
+  e.kind = EPI_ARGMAX; e.keys = s->keys; e.ldo = n; e.col_offset = s->hv0;
+  linear(s, st, xn, s->hw, B, n, s->d.hidden, e, 0);
+  launch_argmax_finalize(s->keys, B, n / 16, (const unsigned long long*)keys_in, (unsigned long long*)keys_out,
+                         tokens, st);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return fail(BS_ERR_DEVICE, std::string("head_slice: ") + hipGetErrorString(err));
   return BS_OK;
 }
 

@@ -35,58 +35,128 @@ class StageExecutor:
         self.stage.forward(inp, out, batch, seq, slot=slot, past_len=past_len,
                            stream=torch.cuda.current_stream().cuda_stream)
 
+    def head_norm(self, hidden, batch, seq, xn):
+        self.stage.head_norm(hidden, batch, seq, xn, stream=torch.cuda.current_stream().cuda_stream)
+
+    def head_slice(self, xn, batch, keys_in, keys_out, tokens):
+        self.stage.head_slice(xn, batch, keys_in, keys_out, tokens, stream=torch.cuda.current_stream().cuda_stream)
+
+
+def vocab_slices(vocab, world):
+    """Contiguous 16-aligned vocabulary slices, one per rank (the vocabulary-parallel head)."""
+    per = ((vocab + world - 1) // world + 15) // 16 * 16
+    return [(min(vocab, r * per), min(vocab, (r + 1) * per)) for r in range(world)]
+
+
+def _is_gloo():
+    return dist.is_initialized() and dist.get_backend() == "gloo"
+
+
+def _recv(buf, src, group=None):
+    if _is_gloo():
+        dist.recv(buf, src=src, group=group)
+    else:
+        dist.irecv(buf, src=src, group=group).wait()  # stream-level wait on the current stream
+
 
 class Pipeline:
     """Static pipeline schedule for one rank.
 
-    rank 0 feeds prompt / token ids, rank N-1 returns token ids to rank 0.  With world == 1
-    the single stage loops its own tokens back (no communication)."""
+    Layer chain: rank 0 feeds prompt / token ids, hidden states go rank -> rank+1.
+    Token pick, two modes:
+      head_split=False: the last rank holds the whole lm_head and returns int32 tokens to rank 0
+                        (on `tok_group`).
+      head_split=True : every rank holds a V/N slice of the tied lm_head.  The last rank computes
+                        ln_f -> xn and its slice's argmax keys, and the (xn, keys) pair travels the
+                        head ring N-1 -> 0 -> 1 -> ... -> N-2 on `head_group` (its own stream); the
+                        rank closing the ring decodes the token and returns it to rank 0 (on
+                        `tok_group`, or locally when that rank is 0).  The layer assignment is
+                        unchanged; the per-rank head work is 1/N of the lm_head.
+    With world == 1 the single stage loops its own tokens back (no communication)."""
 
     def __init__(self, executor, *, rank, world, hidden, mb_rows, n_mb, device, is_first, is_last,
-                 tok_group=None, max_seq=1):
+                 tok_group=None, head_group=None, head_split=False, act_dtype=torch.float32, max_seq=1):
         self.ex, self.rank, self.world = executor, rank, world
         self.h, self.mb, self.n_mb, self.dev = hidden, mb_rows, n_mb, device
         self.is_first, self.is_last = is_first, is_last
-        self.tok_group = tok_group
+        self.tok_group, self.head_group = tok_group, head_group
+        self.head_split = head_split and world > 1
         f32, i32 = torch.float32, torch.int32
         self.hin = [torch.empty(mb_rows * max_seq * hidden, dtype=f32, device=device) for _ in range(n_mb)]
         self.hout = [torch.empty(mb_rows * max_seq * hidden, dtype=f32, device=device) for _ in range(n_mb)]
         self.tok = [torch.zeros(mb_rows, dtype=i32, device=device) for _ in range(n_mb)]
         self.pending = [[] for _ in range(n_mb)]
+        self.hpending = [[] for _ in range(n_mb)]
         self.past = [0] * n_mb
+        if self.head_split:
+            self.xn = [torch.empty(mb_rows * hidden, dtype=act_dtype, device=device) for _ in range(n_mb)]
+            self.kin = [torch.zeros(mb_rows, dtype=torch.int64, device=device) for _ in range(n_mb)]
+            self.kout = [torch.zeros(mb_rows, dtype=torch.int64, device=device) for _ in range(n_mb)]
+            cuda = device.type == "cuda"
+            self.hstream = torch.cuda.Stream(device) if cuda else None
+            self.tok_ready = [torch.cuda.Event() for _ in range(n_mb)] if cuda else None
+            self.closer = world - 2  # rank whose slice closes the head ring
 
-    def _drain(self, j):
-        for w in self.pending[j]:
+    @staticmethod
+    def _drain(lst):
+        for w in lst:
             w.wait()
-        self.pending[j] = []
+        lst.clear()
+
+    # -- head ring (head_split) -------------------------------------------------------
+    def _hctx(self):
+        return torch.cuda.stream(self.hstream) if self.hstream is not None else _nullctx()
+
+    def _head_role(self, j, record):
+        """Ranks 0..N-2: receive (xn, keys) from the previous ring rank, fold in this slice, pass on."""
+        prev = self.world - 1 if self.rank == 0 else self.rank - 1
+        with self._hctx():
+            self._drain(self.hpending[j])
+            _recv(self.xn[j], prev, self.head_group)
+            _recv(self.kin[j], prev, self.head_group)
+            if self.rank == self.closer:
+                self.ex.head_slice(self.xn[j], self.mb, self.kin[j], None, self.tok[j])
+                if self.rank == 0:
+                    if self.tok_ready is not None:
+                        self.tok_ready[j].record()
+                else:
+                    self.hpending[j].append(dist.isend(self.tok[j], dst=0, group=self.tok_group))
+            else:
+                self.ex.head_slice(self.xn[j], self.mb, self.kin[j], self.kout[j], None)
+                self.hpending[j].append(dist.isend(self.xn[j], dst=self.rank + 1, group=self.head_group))
+                self.hpending[j].append(dist.isend(self.kout[j], dst=self.rank + 1, group=self.head_group))
+
+    def _token_in(self, j, record):
+        """Rank 0: the token of micro-batch j from the previous round."""
+        if self.world == 1:
+            return
+        if self.head_split and self.closer == 0:
+            if self.tok_ready is not None:
+                torch.cuda.current_stream().wait_event(self.tok_ready[j])
+        else:
+            src = self.closer if self.head_split else self.world - 1
+            _recv(self.tok[j], src, self.tok_group)
+        if record is not None:
+            record[j].append(self.tok[j].clone())
 
     def step(self, seq, prompt=None, record=None):
         """One pipeline round: every micro-batch advances by `seq` tokens (seq = prompt length
         on the prefill round, 1 on decode rounds).  `prompt` [n_mb*mb, seq] int32 on rank 0
         for the prefill round; rank 0 appends the tokens it receives to `record`."""
         n_el = self.mb * seq * self.h
-        last_rank = self.world - 1
         for j in range(self.n_mb):
             slot = j * self.mb
-            self._drain(j)
+            self._drain(self.pending[j])
             if self.is_first:
                 if prompt is not None:
                     inp = prompt[j * self.mb:(j + 1) * self.mb].contiguous()
                 else:
-                    if self.world > 1:
-                        dist.recv(self.tok[j], src=last_rank, group=self.tok_group) if _is_gloo() else \
-                            dist.irecv(self.tok[j], src=last_rank, group=self.tok_group).wait()
-                        if record is not None:
-                            record[j].append(self.tok[j].clone())
+                    self._token_in(j, record)
                     inp = self.tok[j]
             else:
-                buf = self.hin[j][:n_el]
-                if _is_gloo():
-                    dist.recv(buf, src=self.rank - 1)
-                else:
-                    dist.irecv(buf, src=self.rank - 1).wait()
-                inp = buf
-            if self.is_last:
+                inp = self.hin[j][:n_el]
+                _recv(inp, self.rank - 1)
+            if self.is_last and not self.head_split:
                 self.ex.forward(inp, self.tok[j], self.mb, seq, slot, self.past[j])
                 if self.world > 1:
                     self.pending[j].append(dist.isend(self.tok[j], dst=0, group=self.tok_group))
@@ -95,25 +165,35 @@ class Pipeline:
             else:
                 out = self.hout[j][:n_el]
                 self.ex.forward(inp, out, self.mb, seq, slot, self.past[j])
-                self.pending[j].append(dist.isend(out, dst=self.rank + 1))
+                if not self.is_last:
+                    self.pending[j].append(dist.isend(out, dst=self.rank + 1))
+                else:  # head_split: open the head ring with ln_f and this rank's slice
+                    self.ex.head_norm(out, self.mb, seq, self.xn[j])
+                    self.ex.head_slice(self.xn[j], self.mb, None, self.kout[j], None)
+                    self.pending[j].append(dist.isend(self.xn[j], dst=0, group=self.head_group))
+                    self.pending[j].append(dist.isend(self.kout[j], dst=0, group=self.head_group))
+            if self.head_split and self.rank <= self.closer:
+                self._head_role(j, record)
             self.past[j] += seq
 
     def finish(self, record=None):
         """Rank 0 collects the tokens of the last round; everyone drains its sends."""
         if self.is_first and self.world > 1:
             for j in range(self.n_mb):
-                if _is_gloo():
-                    dist.recv(self.tok[j], src=self.world - 1, group=self.tok_group)
-                else:
-                    dist.irecv(self.tok[j], src=self.world - 1, group=self.tok_group).wait()
-                if record is not None:
-                    record[j].append(self.tok[j].clone())
+                self._token_in(j, record)
         for j in range(self.n_mb):
-            self._drain(j)
+            self._drain(self.pending[j])
+            self._drain(self.hpending[j])
+        if self.head_split and self.hstream is not None:
+            torch.cuda.current_stream().wait_stream(self.hstream)
 
 
-def _is_gloo():
-    return dist.is_initialized() and dist.get_backend() == "gloo"
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def generate(pipe: Pipeline, prompt, steps, prompt_len):
@@ -148,22 +228,32 @@ def init_distributed(backend=None):
 
 
 def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb_rows=1, n_mb=None, max_ctx=1024,
-               max_seq=512, seed=0, executor_factory=None):
-    """Create this rank's stage (server.py:893-905 layer range) and its Pipeline."""
-    n_mb = world if n_mb is None else n_mb
+               max_seq=512, seed=0, head_split=None, executor_factory=None):
+    """Create this rank's stage (server.py:893-905 layer range, plus a vocabulary slice of the
+    tied lm_head when head_split) and its Pipeline.  Collective: every rank must call it."""
+    head_split = (world > 1) if head_split is None else (head_split and world > 1)
+    n_mb = (2 * world if head_split else world) if n_mb is None else n_mb
     lb, le = stage_ranges(world, model.n_layer)[rank]
+    is_first, is_last = rank == 0, rank == world - 1
+    hslice = vocab_slices(model.vocab, world)[rank] if head_split else None
     if executor_factory is None:
         from .stage import Stage
         st = Stage(model.hidden, model.n_head, model.n_layer, model.vocab, lb, le, dtype=dtype,
                    device=device.index if device.type == "cuda" else 0, max_batch=mb_rows * n_mb,
-                   max_ctx=max_ctx, max_tokens=mb_rows * max_seq, seed=seed, is_first=(rank == 0),
-                   is_last=(rank == world - 1))
+                   max_ctx=max_ctx, max_tokens=mb_rows * max_seq, seed=seed, is_first=is_first,
+                   is_last=is_last and not head_split, head_slice=hslice)
         ex = StageExecutor(st)
     else:
-        ex = executor_factory(lb, le, rank == 0, rank == world - 1, mb_rows * n_mb, max_ctx)
-    tok_group = dist.new_group(ranks=sorted({0, world - 1})) if world > 1 else None
+        ex = executor_factory(lb, le, is_first, is_last and not head_split, mb_rows * n_mb, max_ctx, hslice)
+    # communicators are created collectively, in the same order on every rank
+    tok_group = head_group = None
+    if world > 1:
+        tok_group = dist.new_group(ranks=list(range(world)))
+        head_group = dist.new_group(ranks=list(range(world)))
+    act = torch.bfloat16 if dtype == "bf16" else torch.float32
     pipe = Pipeline(ex, rank=rank, world=world, hidden=model.hidden, mb_rows=mb_rows, n_mb=n_mb, device=device,
-                    is_first=(rank == 0), is_last=(rank == world - 1), tok_group=tok_group, max_seq=max_seq)
+                    is_first=is_first, is_last=is_last, tok_group=tok_group, head_group=head_group,
+                    head_split=head_split, act_dtype=act, max_seq=max_seq)
     return pipe, (lb, le)
 
 
@@ -173,14 +263,16 @@ def bench_pipeline(args):
     dev = torch.device("cuda", local)
     model = config.get(args.model)
     B, P, K, W = args.batch, args.prompt, args.steps, args.warmup
-    pipe, (lb, le) = build_rank(model, rank, world, dev, dtype=args.dtype, mb_rows=B, n_mb=world,
-                                max_ctx=P + W + K + 2, max_seq=P, seed=args.seed)
+    head_split = not getattr(args, "no_head_split", False)
+    pipe, (lb, le) = build_rank(model, rank, world, dev, dtype=args.dtype, mb_rows=B, max_ctx=P + W + K + 2,
+                                max_seq=P, seed=args.seed, head_split=head_split)
+    n_mb = pipe.n_mb
     cs = torch.cuda.Stream()  # a real stream: decode steps are captured as hipGraphs
     torch.cuda.set_stream(cs)
     prompt = None
     if rank == 0:
         from .stage import prompt_ids
-        prompt = torch.from_numpy(prompt_ids(1234, B * world, P, model.vocab)).to(dev)
+        prompt = torch.from_numpy(prompt_ids(1234, B * n_mb, P, model.vocab)).to(dev)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -204,16 +296,18 @@ def bench_pipeline(args):
     per_stage = [b - a for a, b in stage_ranges(world, model.n_layer)]
     res = None
     if rank == 0:
-        toks = B * world * K
+        toks = B * n_mb * K
         res = {
             "metric": "decode tokens/s, BLOOM pipeline", "value": toks / dt, "unit": "tokens/s", "n_gpus": world,
             "steps": K, "warmup": W, "ms_per_step": dt * 1e3 / K, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic: repo-generator random-init weights (seed %d), prompt ids U[0,V) seed 1234" % args.seed,
             "config": {"workload": f"{model.name} split into {world} stages by the server's round-robin layer "
-                                   f"assignment, {world} micro-batches x {B} rows in flight, RCCL send/recv",
-                       "model": model.name, "stages": world, "layers_per_stage": per_stage, "batch": B * world,
-                       "micro_batch": B, "prompt": P, "parallelism": f"pp{world}"},
+                                   f"assignment, {n_mb} micro-batches x {B} rows in flight, RCCL send/recv"
+                                   + (", vocabulary-parallel lm_head ring" if pipe.head_split else ""),
+                       "model": model.name, "stages": world, "layers_per_stage": per_stage, "batch": B * n_mb,
+                       "micro_batch": B, "prompt": P, "parallelism": f"pp{world}",
+                       "head": "vocab-split ring" if pipe.head_split else "last stage"},
             "prefill_plus_warmup_s": t_prefill_warm,
         }
     dist.barrier()

@@ -59,6 +59,7 @@ class StageDesc(ctypes.Structure):
         ("max_batch", ctypes.c_int32), ("max_ctx", ctypes.c_int32), ("max_tokens", ctypes.c_int32),
         ("weight_source", ctypes.c_int32), ("seed", ctypes.c_uint64),
         ("host_weights", ctypes.c_void_p), ("host_weight_count", ctypes.c_uint64),
+        ("head_vocab_begin", ctypes.c_int32), ("head_vocab_end", ctypes.c_int32),
         ("flags", ctypes.c_int32),
     ]
 
@@ -77,7 +78,7 @@ EXPORTS = [
     "bs_init_stage", "bs_forward", "bs_reset_kv", "bs_release", "bs_last_error", "bs_stage_info",
     "bs_stage_weight_count", "bs_abi_version", "bs_profile_enable", "bs_profile_read",
     "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
-    "bs_prompt_ids", "bs_read_weights",
+    "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice",
 ]
 
 _LIB = None
@@ -113,6 +114,8 @@ def lib():
         L.bs_deserialize_int.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(i32)]
         L.bs_prompt_ids.argtypes = [ctypes.c_uint64, i32, i32, vp]
         L.bs_read_weights.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, vp]
+        L.bs_head_norm.argtypes = [vp, vp, i32, i32, vp, vp]
+        L.bs_head_slice.argtypes = [vp, vp, i32, vp, vp, vp, vp]
         _LIB = L
     return _LIB
 
@@ -139,7 +142,7 @@ class Stage:
 
     def __init__(self, hidden, n_head, n_layer, vocab, layer_begin, layer_end, *, dtype="bf16", device=0,
                  max_batch=1, max_ctx=2048, max_tokens=0, seed=0, eps=1e-5, host_weights=None,
-                 is_first=None, is_last=None):
+                 is_first=None, is_last=None, head_slice=None):
         d = StageDesc()
         d.hidden, d.n_head, d.n_layer, d.vocab, d.ln_eps = hidden, n_head, n_layer, vocab, eps
         d.layer_begin, d.layer_end = layer_begin, layer_end
@@ -148,6 +151,8 @@ class Stage:
         d.dtype = BS_DT_BFLOAT16 if dtype in ("bf16", BS_DT_BFLOAT16) else BS_DT_FLOAT
         d.device, d.max_batch, d.max_ctx, d.max_tokens = device, max_batch, max_ctx, max_tokens
         d.seed = seed
+        if head_slice is not None:
+            d.head_vocab_begin, d.head_vocab_end = head_slice
         self._weights_ref = None
         if host_weights is not None:
             w = np.ascontiguousarray(host_weights, dtype=np.float32).reshape(-1)
@@ -175,6 +180,15 @@ class Stage:
         for r in range(slot, slot + batch):
             self.past[r] = past + seq
         return out
+
+    # ---- vocabulary-parallel head (device pointers, stream ordered)
+    def head_norm(self, hidden, batch, seq, xn, stream=None):
+        """ln_f of each row's last position -> xn [batch][hidden] (stage activation dtype)."""
+        _check(lib().bs_head_norm(self._h, _ptr(hidden), batch, seq, _ptr(xn), stream))
+
+    def head_slice(self, xn, batch, keys_in=None, keys_out=None, tokens=None, stream=None):
+        """Argmax keys of this stage's vocabulary slice, merged with keys_in (uint64 [batch])."""
+        _check(lib().bs_head_slice(self._h, _ptr(xn), batch, _ptr(keys_in), _ptr(keys_out), _ptr(tokens), stream))
 
     # ---- host I/O convenience (numpy in, numpy out)
     def forward_host(self, x, batch, seq, slot=0, past_len=None, want_logits=False):

@@ -79,6 +79,10 @@ typedef struct bs_stage_desc {
   uint64_t seed;         /* BS_WEIGHTS_SYNTHETIC */
   const float *host_weights;  /* BS_WEIGHTS_HOST */
   uint64_t host_weight_count; /* floats in host_weights */
+  /* vocabulary-parallel head slice: lm_head rows [head_vocab_begin, head_vocab_end) + ln_f
+   * (0, 0 = none).  Used by pipelines that spread the tied lm_head over all stages. */
+  int32_t head_vocab_begin;
+  int32_t head_vocab_end;
   int32_t flags;         /* reserved, 0 */
 } bs_stage_desc;
 
@@ -108,6 +112,18 @@ int bs_init_stage(const bs_stage_desc *desc, bs_stage **out);
 int bs_forward(bs_stage *stage, const bs_step *step, const void *in, void *out, float *logits,
                void *stream);
 
+/* ---- Vocabulary-parallel head (stages with a head slice, or the last stage) ----
+ * Argmax keys: uint64 (order(logit) << 32) | (0xFFFFFFFF - vocab_index), where order() maps
+ * fp32 monotonically to uint32; the max key is the greedy token (lowest index on ties). */
+/* ln_f of each row's last position: hidden fp32 [B][S][hidden] -> xn [B][hidden] in the stage's
+ * activation type (bf16 for BS_DT_BFLOAT16 stages, fp32 otherwise). */
+int bs_head_norm(bs_stage *stage, const float *hidden, int32_t batch, int32_t seq, void *xn, void *stream);
+/* Logits of the stage's vocabulary slice for xn [B][hidden]; writes per-row keys
+ * max(keys_in[b], slice max) to keys_out (either may be NULL) and, when tokens is non-NULL,
+ * the decoded token ids.  Device pointers, stream ordered. */
+int bs_head_slice(bs_stage *stage, const void *xn, int32_t batch, const uint64_t *keys_in, uint64_t *keys_out,
+                  int32_t *tokens, void *stream);
+
 /* Forget the cached positions of one KV row (slot), or of all rows when slot < 0. */
 int bs_reset_kv(bs_stage *stage, int32_t slot);
 
@@ -118,7 +134,11 @@ const char *bs_last_error(void);
 /* Introspection */
 int bs_stage_info(const bs_stage *stage, bs_stage_desc *out_desc, uint64_t *weight_bytes,
                   uint64_t *kv_bytes, uint64_t *workspace_bytes);
-uint64_t bs_stage_weight_count(const bs_stage_desc *desc); /* fp32 count for BS_WEIGHTS_HOST */
+/* fp32 count for BS_WEIGHTS_HOST.  Canonical order: [word_embeddings if first or last]
+ * [emb LN g,b if first]{per layer: ln1 g,b, qkv w,b, dense w,b, ln2 g,b, fc1 w,b, fc2 w,b}
+ * [ln_f g,b if last][head slice rows if a slice is set and the stage is neither first nor last]
+ * [ln_f g,b if a slice is set and the stage is not last]. */
+uint64_t bs_stage_weight_count(const bs_stage_desc *desc);
 int bs_abi_version(void);
 /* Read back `count` weights starting at element `offset` of the canonical stage order
  * (the BS_WEIGHTS_HOST layout) as fp32.  For verification of loaded/generated weights. */

@@ -310,6 +310,43 @@ int or_forward(or_stage *s, int B, int S, int slot, int past_len, const void *in
   return 0;
 }
 
+/* Vocabulary-parallel head, restating the tail of the forward above for a vocab slice:
+ * xn[b] = ln_f(hidden[b][S-1]) (bf16-rounded in bf16 mode); keys = max over the slice rows
+ * [v0, v1) of (order(logit) << 32 | (0xFFFFFFFF - v)), merged with keys_in. */
+int or_head_norm(or_stage *s, const float *hidden, int B, int S, float *xn) {
+  if (!s->lnf_g || !s->wemb) return -1;
+  float *rows = (float *)malloc(sizeof(float) * (size_t)B * s->h);
+  for (int b = 0; b < B; b++) memcpy(rows + (size_t)b * s->h, hidden + ((size_t)b * S + S - 1) * s->h, sizeof(float) * s->h);
+  layernorm(rows, xn, B, s->h, s->lnf_g, s->lnf_b, s->eps, 1, s);
+  free(rows);
+  return 0;
+}
+
+static uint64_t order_key(float f, uint32_t v) {
+  union { float f; uint32_t u; } x; x.f = f;
+  uint32_t k = (x.u & 0x80000000u) ? ~x.u : (x.u | 0x80000000u);
+  return ((uint64_t)k << 32) | (0xFFFFFFFFu - v);
+}
+
+int or_head_slice(or_stage *s, const float *xn, int B, int v0, int v1, const uint64_t *keys_in, uint64_t *keys_out,
+                  int32_t *tokens) {
+  if (!s->wemb || v0 < 0 || v1 > s->V || v0 >= v1) return -1;
+  int n = v1 - v0;
+  float *lg = (float *)malloc(sizeof(float) * (size_t)B * n);
+  linear(xn, s->wemb + (size_t)v0 * s->h, NULL, lg, B, n, s->h);
+  for (int b = 0; b < B; b++) {
+    uint64_t best = keys_in ? keys_in[b] : 0;
+    for (int v = 0; v < n; v++) {
+      uint64_t k = order_key(lg[(size_t)b * n + v], (uint32_t)(v0 + v));
+      if (k > best) best = k;
+    }
+    if (keys_out) keys_out[b] = best;
+    if (tokens) tokens[b] = (int32_t)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu));
+  }
+  free(lg);
+  return 0;
+}
+
 /* Copy of one KV row for tests: which 0=K 1=V, layer index local to the stage. */
 int or_read_kv(const or_stage *s, int li, int which, int row, int head, int pos, float *out) {
   if (li < 0 || li >= s->le - s->lb) return -1;

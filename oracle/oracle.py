@@ -28,6 +28,9 @@ def lib():
         L.or_read_kv.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p]
         L.or_num_threads.restype = ctypes.c_int
         L.or_set_accum_double.argtypes = [ctypes.c_int]
+        L.or_head_norm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.or_head_slice.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         _LIB = L
     return _LIB
 
@@ -82,6 +85,22 @@ class OracleStage:
         if rc != 0:
             raise ValueError(f"or_forward failed rc={rc}")
         return (out, logits) if want_logits else out
+
+    def head_norm(self, hidden, B, S):
+        hidden = np.ascontiguousarray(hidden, dtype=np.float32).reshape(B, S, self.hidden)
+        xn = np.empty((B, self.hidden), np.float32)
+        if lib().or_head_norm(self.h, _p(hidden), B, S, _p(xn)) != 0:
+            raise ValueError("or_head_norm needs a stage with the head (is_last)")
+        return xn
+
+    def head_slice(self, xn, B, v0, v1, keys_in=None):
+        xn = np.ascontiguousarray(xn, dtype=np.float32).reshape(B, self.hidden)
+        keys = np.empty(B, np.uint64)
+        toks = np.empty(B, np.int32)
+        kin = None if keys_in is None else np.ascontiguousarray(keys_in, dtype=np.uint64)
+        if lib().or_head_slice(self.h, _p(xn), B, v0, v1, _p(kin), _p(keys), _p(toks)) != 0:
+            raise ValueError("or_head_slice failed")
+        return keys, toks
 
     def read_kv(self, layer_local, which, row, head, pos, head_dim):
         out = np.empty(head_dim, dtype=np.float32)

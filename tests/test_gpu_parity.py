@@ -270,3 +270,23 @@ def test_graph_and_eager_paths_agree_bitwise():
     # the MFMA GEMV (used for M > 4) and the row-streaming GEMV (M <= 4) agree to bf16 tolerance
     c = np.load(os.path.join(d, "mfma.npy"))
     assert np.abs(a - c).max() <= 2e-2
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_split_kv_decode_attention(dtype):
+    """B*heads small and max_ctx large: the context is split over several blocks and merged;
+    short contexts leave trailing splits empty."""
+    h, nh, L, V, B = 256, 4, 1, 1024, 1
+    gs, os_ = pair(h, nh, L, V, 0, L, dtype, seed=33, max_batch=B, max_ctx=1100, max_tokens=700, is_last=False)
+    ids = gen_np.prompt_ids(4, B, 700, V).astype(np.int32)
+    # short prompt -> decode: one chunk, empty splits
+    check_close(gs.forward_host(ids[:, :5], B, 5, past_len=0), os_.forward(ids[:, :5], B, 5, past_len=0), dtype, "p5")
+    for p in (5, 6, 63, 64):
+        check_close(gs.forward_host(ids[:, p:p + 1], B, 1, past_len=p), os_.forward(ids[:, p:p + 1], B, 1, past_len=p),
+                    dtype, f"decode past={p}")
+    # long prefix -> decode across many chunks
+    gs.forward_host(ids[:, 65:700], B, 635, past_len=65)
+    os_.forward(ids[:, 65:700], B, 635, past_len=65)
+    for p in (700, 701):
+        tok = ids[:, (p * 7) % 700:(p * 7) % 700 + 1]
+        check_close(gs.forward_host(tok, B, 1, past_len=p), os_.forward(tok, B, 1, past_len=p), dtype, f"decode past={p}")

@@ -20,10 +20,24 @@ SEED, P, STEPS, MB = 3, 6, 10, 2
 
 
 class OracleExecutor:
-    def __init__(self, lb, le, first, last, max_batch, max_ctx):
+    def __init__(self, lb, le, first, last, max_batch, max_ctx, hslice=None):
         self.st = OracleStage(MODEL.hidden, MODEL.n_head, MODEL.n_layer, MODEL.vocab, lb, le, max_batch=max_batch,
                               max_ctx=max_ctx, seed=SEED, is_first=first, is_last=last)
-        self.first, self.last = first, last
+        self.first, self.last, self.hslice = first, last, hslice
+        if hslice is not None:  # layer-free stage owning the tied head for ln_f + the vocab slice
+            self.head = OracleStage(MODEL.hidden, MODEL.n_head, MODEL.n_layer, MODEL.vocab, 0, 0, max_batch=max_batch,
+                                    max_ctx=max_ctx, seed=SEED, is_first=False, is_last=True)
+
+    def head_norm(self, hidden, batch, seq, xn):
+        xn.copy_(torch.from_numpy(self.head.head_norm(hidden.numpy()[: batch * seq * MODEL.hidden], batch, seq).reshape(-1)))
+
+    def head_slice(self, xn, batch, keys_in, keys_out, tokens):
+        kin = None if keys_in is None else keys_in.numpy().view(np.uint64)
+        keys, toks = self.head.head_slice(xn.numpy(), batch, self.hslice[0], self.hslice[1], kin)
+        if keys_out is not None:
+            keys_out.copy_(torch.from_numpy(keys.view(np.int64)))
+        if tokens is not None:
+            tokens.copy_(torch.from_numpy(toks))
 
     def forward(self, inp, out, batch, seq, slot, past_len):
         x = inp.numpy()
@@ -31,13 +45,13 @@ class OracleExecutor:
         out.copy_(torch.from_numpy(np.ascontiguousarray(y).reshape(-1)[: out.numel()]).view(out.shape))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, head_split=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        pipe, _ = build_rank(MODEL, rank, world, torch.device("cpu"), mb_rows=MB, n_mb=world, max_ctx=P + STEPS + 2,
-                             max_seq=P, executor_factory=OracleExecutor)
-        prompt = torch.from_numpy(prompt_ids(1234, MB * world, P, MODEL.vocab)) if rank == 0 else None
+        pipe, _ = build_rank(MODEL, rank, world, torch.device("cpu"), mb_rows=MB, max_ctx=P + STEPS + 2,
+                             max_seq=P, executor_factory=OracleExecutor, head_split=head_split, dtype="fp32")
+        prompt = torch.from_numpy(prompt_ids(1234, MB * pipe.n_mb, P, MODEL.vocab)) if rank == 0 else None
         toks = generate(pipe, prompt, STEPS, P)
         if rank == 0:
             q.put(toks.numpy())
@@ -54,12 +68,12 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_pipeline_matches_single_stage(world):
+@pytest.mark.parametrize("world,head_split", [(2, False), (3, False), (2, True), (3, True), (4, True)])
+def test_pipeline_matches_single_stage(world, head_split):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, head_split)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
@@ -67,7 +81,8 @@ def test_pipeline_matches_single_stage(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     # single stage reference, all rows at once
-    B = MB * world
+    B = got.shape[0]
+    assert B == MB * world * (2 if head_split else 1)
     ref = OracleStage(MODEL.hidden, MODEL.n_head, MODEL.n_layer, MODEL.vocab, 0, MODEL.n_layer, max_batch=B,
                       max_ctx=P + STEPS + 2, seed=SEED)
     tok = ref.forward(prompt_ids(1234, B, P, MODEL.vocab), B, P)
@@ -80,7 +95,7 @@ def test_pipeline_matches_single_stage(world):
 
 def test_single_rank_pipeline_loops_tokens_back():
     pipe, _ = build_rank(MODEL, 0, 1, torch.device("cpu"), mb_rows=MB, n_mb=2, max_ctx=P + STEPS + 2, max_seq=P,
-                         executor_factory=OracleExecutor)
+                         executor_factory=OracleExecutor, dtype="fp32")
     prompt = torch.from_numpy(prompt_ids(1234, 2 * MB, P, MODEL.vocab))
     got = generate(pipe, prompt, 4, P).numpy()
     ref = OracleStage(MODEL.hidden, MODEL.n_head, MODEL.n_layer, MODEL.vocab, 0, MODEL.n_layer, max_batch=2 * MB,
