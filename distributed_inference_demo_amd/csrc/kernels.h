@@ -5,7 +5,7 @@
 
 // Epilogue of every weight GEMM/GEMV: y[m][n] = sum_k X[m][k] * W[n][k] (+ what `kind` says).
 enum EpiKind : int {
-  EPI_QKV = 0,     // + bias; q -> q_out fp32 [M][h]; k,v -> KV cache (T) at (slot+b, past+t)
+  EPI_QKV = 0,     // + bias; q -> q_out (T) [M][h]; k,v -> KV cache (T) at (slot+b, past+t)
   EPI_RESID = 1,   // out_f32[m][n] = (y + bias) + resid[m][n]
   EPI_GELU = 2,    // out_act[m][n] = T(gelu(y + bias))
   EPI_ARGMAX = 3,  // no bias; 64-bit atomicMax of (order(y), ~n) into keys[m]; optional logits
@@ -19,7 +19,7 @@ struct Epi {
   const float* resid;     // EPI_RESID residual [M][ldo]
   int ldo;                // leading dim of out/resid (= N)
   // EPI_QKV
-  float* q_out;           // [M][hidden]
+  void* q_out;            // T [M][hidden]
   void* k_cache;          // T, layer base of K: [max_batch][heads][max_ctx][hd]
   void* v_cache;
   int hidden, head_dim, max_ctx, n_head;
@@ -55,7 +55,7 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
 
 // Attention over the KV cache for B rows x S new queries per row (causal, ALiBi).
 struct AttnArgs {
-  const float* q;      // [B*S][hidden] fp32
+  const void* q;       // T [B*S][hidden]
   const void* k_cache; // T layer base
   const void* v_cache;
   void* ctx_out;       // T [B*S][hidden]

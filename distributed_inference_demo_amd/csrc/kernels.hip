@@ -161,7 +161,7 @@ __device__ __forceinline__ void epi_store(const Epi& e, int m, int n, float v) {
     const int three = 3 * e.head_dim;
     const int head = n / three, r = n - head * three, which = r / e.head_dim, d = r - which * e.head_dim;
     if (which == 0) {
-      e.q_out[(size_t)m * e.hidden + head * e.head_dim + d] = v;
+      ((T*)e.q_out)[(size_t)m * e.hidden + head * e.head_dim + d] = from_f32<T>(v);
     } else {
       const int b = m / e.seq, t = m - b * e.seq;
       const int past = e.past_dev ? *e.past_dev : e.past;
@@ -667,6 +667,106 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(const bf16* __restrict__
 }
 
 // ------------------------------------------------------------------------------------
+// gemm_mfma2: prefill GEMM, BM x BN tile (64/128 each), BK = 64, 256 threads as 2x2 waves
+// (wave tile BM/2 x BN/2), register-staged double buffer.  LDS rows are 128 B (64 bf16) with the
+// 16-B chunk index XOR-swizzled by (row & 7), so the 16 rows a ds_read_b128 lane group touches
+// land on different chunk slots.  16 (BN=128) or 8 (BN=64) MFMAs per 32-deep k-step per wave.
+// ------------------------------------------------------------------------------------
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
+                                                         int M, int N, int K, Epi ep) {
+  constexpr int BK = 64;
+  constexpr int TM = BM / 32, TN = BN / 32;           // 16x16 tiles per wave (wave = BM/2 x BN/2)
+  constexpr int CA = BM * BK / 8 / 256, CB = BN * BK / 8 / 256;  // 16-B chunks per thread: 4, 4|2
+  __shared__ __attribute__((aligned(16))) bf16 As[2][BM * BK];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * BK];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1, r = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  auto sw = [](int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); };  // element offset
+
+  const bf16* ga[CA]; const bf16* gb[CB];
+  int la[CA], lb[CB];
+#pragma unroll
+  for (int i = 0; i < CA; i++) {
+    const int c = tid + i * 256, row = c >> 3, ch = c & 7;
+    ga[i] = X + (size_t)min(m0 + row, M - 1) * K + ch * 8;
+    la[i] = sw(row, ch);
+  }
+#pragma unroll
+  for (int i = 0; i < CB; i++) {
+    const int c = tid + i * 256, row = c >> 3, ch = c & 7;
+    gb[i] = W + (size_t)min(n0 + row, N - 1) * K + ch * 8;
+    lb[i] = sw(row, ch);
+  }
+  bf16x8 ra[CA], rb[CB];
+#pragma unroll
+  for (int i = 0; i < CA; i++) ra[i] = *reinterpret_cast<const bf16x8*>(ga[i]);
+#pragma unroll
+  for (int i = 0; i < CB; i++) rb[i] = *reinterpret_cast<const bf16x8*>(gb[i]);
+#pragma unroll
+  for (int i = 0; i < CA; i++) *reinterpret_cast<bf16x8*>(&As[0][la[i]]) = ra[i];
+#pragma unroll
+  for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(&Bs[0][lb[i]]) = rb[i];
+  __syncthreads();
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; i++)
+#pragma unroll
+    for (int j = 0; j < TN; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  int cur = 0;
+  for (int kt = 0; kt < nk; kt++) {
+    const bool more = kt + 1 < nk;
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < CA; i++) ra[i] = *reinterpret_cast<const bf16x8*>(ga[i] + (size_t)(kt + 1) * BK);
+#pragma unroll
+      for (int i = 0; i < CB; i++) rb[i] = *reinterpret_cast<const bf16x8*>(gb[i] + (size_t)(kt + 1) * BK);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ks++) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; i++)
+        af[i] = *reinterpret_cast<const bf16x8*>(&As[cur][sw(wm * (BM / 2) + i * 16 + r, ks * 4 + g)]);
+#pragma unroll
+      for (int j = 0; j < TN; j++)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][sw(wn * (BN / 2) + j * 16 + r, ks * 4 + g)]);
+#pragma unroll
+      for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < CA; i++) *reinterpret_cast<bf16x8*>(&As[cur ^ 1][la[i]]) = ra[i];
+#pragma unroll
+      for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(&Bs[cur ^ 1][lb[i]]) = rb[i];
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  const int ntiles = (N + 15) >> 4;
+  epi_dispatch(ep.kind, [&](auto kc) {
+    constexpr int EK = decltype(kc)::value;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+      for (int j = 0; j < TN; j++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const int m = m0 + wm * (BM / 2) + i * 16 + 4 * g + e;
+          const int n = n0 + wn * (BN / 2) + j * 16 + r;
+          epi_apply<bf16, EK>(ep, m, n, acc[i][j][e], m < M && n < N, ntiles);
+        }
+  });
+}
+
+// ------------------------------------------------------------------------------------
 // gemm_f32: exact-fp32 path (parity mode).  16x16 output tile per 256-thread block.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ X, const float* __restrict__ W,
@@ -689,6 +789,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   epi_dispatch(ep.kind, [&](auto kc) {
     epi_apply<float, decltype(kc)::value>(ep, m, n, acc, m < M && n < N, (N + 15) >> 4);
   });
+}
+
+static bool gemm_v1_forced() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("BS_GEMM_V1"); v = (e && *e && *e != '0') ? 1 : 0; }
+  return v == 1;
 }
 
 static bool gemv_rows_disabled() {
@@ -781,6 +887,18 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
     gemv_dispatch<false>(x, LnArgs{}, w, M, N, K, ep, s);
     return;
   }
+  if ((K % 64) == 0 && !gemm_v1_forced()) {
+    // largest tile that still gives every CU a block (>= 240 blocks), else the smallest
+    auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+    if (blocks(128, 128) >= 240) {
+      gemm_mfma2_kernel<128, 128><<<dim3((N + 127) / 128, (M + 127) / 128), 256, 0, s>>>(x, w, M, N, K, ep);
+    } else if (blocks(128, 64) >= 240) {
+      gemm_mfma2_kernel<128, 64><<<dim3((N + 63) / 64, (M + 127) / 128), 256, 0, s>>>(x, w, M, N, K, ep);
+    } else {
+      gemm_mfma2_kernel<64, 64><<<dim3((N + 63) / 64, (M + 63) / 64), 256, 0, s>>>(x, w, M, N, K, ep);
+    }
+    return;
+  }
   const long big = (long)((M + 127) / 128) * ((N + 127) / 128);
   if (big >= 256) {
     dim3 grid((N + 127) / 128, (M + 127) / 128);
@@ -811,7 +929,7 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int head = blockIdx.x, b = blockIdx.y, sp = blockIdx.z, nsplit = gridDim.z;
   const int hd = a.head_dim;
-  for (int d = threadIdx.x; d < hd; d += WV * 64) qs[d] = a.q[(size_t)b * a.hidden + head * hd + d];
+  for (int d = threadIdx.x; d < hd; d += WV * 64) qs[d] = to_f32(((const T*)a.q)[(size_t)b * a.hidden + head * hd + d]);
   __syncthreads();
   const int past = a.past_dev ? *a.past_dev : a.past;
   const int nk = past + 1, nlast = nk - 1;
@@ -943,7 +1061,7 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(AttnArgs a) {
   const int past = a.past_dev ? *a.past_dev : a.past;
   const int nk = past + t + 1;
   const int m = b * a.S + t;
-  for (int d = lane; d < hd; d += 64) qs[d] = a.q[(size_t)m * a.hidden + head * hd + d];
+  for (int d = lane; d < hd; d += 64) qs[d] = to_f32(((const T*)a.q)[(size_t)m * a.hidden + head * hd + d]);
   __syncthreads();
   const size_t rowbase = ((size_t)(a.slot + b) * a.n_head + head) * a.max_ctx;
   const T* kb = (const T*)a.k_cache + rowbase * hd;
@@ -983,6 +1101,151 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(AttnArgs a) {
   if (lane + 64 < hd) o[lane + 64] = from_f32<T>(acc1 * inv);
 }
 
+// Prefill (S > 1), bf16: MFMA flash attention.  Block = (64-query tile, head, row b), 4 waves x 16
+// queries.  Per 32-key tile: K rows and V^T staged in LDS by the block; S = Q.K^T on
+// v_mfma_f32_16x16x32_bf16 (Q fragments in registers, zero-padded past hd); scale + ALiBi +
+// causal mask + online softmax on the accumulator layout (row = 4*(lane>>4)+i, key = lane&15);
+// P -> fp16 through LDS into the A operand of the P.V MFMAs (v_mfma_f32_16x16x32_f16; V is staged
+// as fp16 — exact for bf16 values in fp16's normal range — so P keeps 10 mantissa bits instead of 7).
+// q is bf16 (the stage stores q in the activation dtype); accumulation and softmax fp32.
+template <int HDP>  // head_dim padded to a multiple of 32 (64, 96, 128)
+__global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
+  constexpr int KT = 32;                 // keys per tile
+  constexpr int KS = HDP / 32;           // k-steps of S = Q.K^T
+  constexpr int NT = HDP / 16;           // 16-dim output tiles
+  constexpr int KLD = HDP + 8;           // padded K row (bf16 elements)
+  constexpr int VLD = KT + 8;            // padded V^T row
+  __shared__ __attribute__((aligned(16))) bf16 Ks[KT * KLD];
+  __shared__ __attribute__((aligned(16))) _Float16 Vt[HDP * VLD];
+  __shared__ __attribute__((aligned(16))) _Float16 Ps[4][16 * VLD];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const int qt = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
+  const int hd = a.head_dim;
+  const int past = a.past_dev ? *a.past_dev : a.past;
+  const int q0 = qt * 64 + w * 16;          // first query (within this call) of the wave
+  const bf16* qg = (const bf16*)a.q;
+  // Q fragments: lane holds Q[q0 + r][ks*32 + 8g .. +8]
+  bf16x8 qf[KS];
+  {
+    const int qrow = min(q0 + r, a.S - 1);
+    const bf16* qp = qg + ((size_t)b * a.S + qrow) * a.hidden + head * hd;
+#pragma unroll
+    for (int ks = 0; ks < KS; ks++) {
+      const int d = ks * 32 + 8 * g;
+      qf[ks] = d < hd ? *reinterpret_cast<const bf16x8*>(qp + d) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  const size_t rowbase = ((size_t)(a.slot + b) * a.n_head + head) * a.max_ctx;
+  const bf16* kb = (const bf16*)a.k_cache + rowbase * hd;
+  const bf16* vb = (const bf16*)a.v_cache + rowbase * hd;
+  const float slope = a.slopes[head];
+  float m_run[4], l_run[4];
+  f32x4 o[NT];
+#pragma unroll
+  for (int i = 0; i < 4; i++) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
+#pragma unroll
+  for (int t = 0; t < NT; t++) o[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // keys visible to the block's last query
+  const int kend = past + min(a.S, qt * 64 + 64);
+  const int nchunk = hd / 8;
+  for (int k0 = 0; k0 < kend; k0 += KT) {
+    __syncthreads();  // previous tile's LDS reads are done
+    // stage K rows and V^T: 32 keys x hd, 16-B chunks
+    for (int c = tid; c < KT * nchunk; c += 256) {
+      const int kr = c / nchunk, dc = (c - kr * nchunk) * 8;
+      const int key = min(k0 + kr, kend - 1);
+      const bf16x8 kv = *reinterpret_cast<const bf16x8*>(kb + (size_t)key * hd + dc);
+      *reinterpret_cast<bf16x8*>(&Ks[kr * KLD + dc]) = kv;
+      const bf16x8 vv = *reinterpret_cast<const bf16x8*>(vb + (size_t)key * hd + dc);
+#pragma unroll
+      for (int j = 0; j < 8; j++) Vt[(dc + j) * VLD + kr] = (_Float16)(float)vv[j];
+    }
+    if (HDP != 0) {  // zero the padded dims once per tile (cheap; keeps the MFMA inputs finite)
+      for (int c = tid; c < KT * (HDP - hd); c += 256) {
+        const int kr = c / (HDP - hd), d = hd + (c - kr * (HDP - hd));
+        Ks[kr * KLD + d] = (bf16)0.f;
+        Vt[d * VLD + kr] = (_Float16)0.f;
+      }
+    }
+    __syncthreads();
+    // S tiles: two 16-key tiles
+    f32x4 sacc[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ks++) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(t * 16 + r) * KLD + ks * 32 + 8 * g]);
+        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, sacc[t], 0, 0, 0);
+      }
+    }
+    // scale, ALiBi, causal mask; lane holds rows 4g+i, key t*16 + r
+    float sv[2][4], rmax[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int qpos = past + q0 + 4 * g + i;
+      rmax[i] = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        const int kpos = k0 + t * 16 + r;
+        const float v = (kpos <= qpos && kpos < kend) ? slope * (float)kpos + a.inv_norm * sacc[t][i] : -INFINITY;
+        sv[t][i] = v;
+        rmax[i] = fmaxf(rmax[i], v);
+      }
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1) rmax[i] = fmaxf(rmax[i], __shfl_xor(rmax[i], off, 64));
+    }
+    float scale[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const float m_new = fmaxf(m_run[i], rmax[i]);
+      // rows whose keys are all masked so far keep m = -inf; exp(-inf - -inf) guarded
+      scale[i] = m_new == -INFINITY ? 1.f : __expf(m_run[i] - m_new);
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        const float p = m_new == -INFINITY ? 0.f : __expf(sv[t][i] - m_new);
+        sv[t][i] = p;
+        rs += p;
+      }
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
+      l_run[i] = l_run[i] * scale[i] + rs;
+      m_run[i] = m_new;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; t++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) o[t][i] *= scale[i];
+    // P -> LDS (bf16, [16 q][32 keys]) -> A fragment
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) Ps[w][(4 * g + i) * VLD + t * 16 + r] = (_Float16)sv[t][i];
+    __builtin_amdgcn_wave_barrier();
+    typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+    const f16x8 pf = *reinterpret_cast<const f16x8*>(&Ps[w][r * VLD + 8 * g]);
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      const f16x8 vf = *reinterpret_cast<const f16x8*>(&Vt[(t * 16 + r) * VLD + 8 * g]);
+      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, vf, o[t], 0, 0, 0);
+    }
+  }
+  // write ctx rows (q = q0 + 4g + i, dim = t*16 + r)
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int q = q0 + 4 * g + i;
+    if (q >= a.S) continue;
+    const float inv = 1.0f / l_run[i];
+    bf16* op = (bf16*)a.ctx_out + ((size_t)b * a.S + q) * a.hidden + head * hd;
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      const int d = t * 16 + r;
+      if (d < hd) op[d] = (bf16)(o[t][i] * inv);
+    }
+  }
+}
+
 size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, int* max_chunks, int* chunk) {
   const int ch = 64;  // == the wave width of attn_decode_kernel
   const int mc = (max_ctx + ch - 1) / ch;
@@ -1017,9 +1280,17 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
       }
     }
   } else {
-    dim3 g(a.S, a.n_head, a.B);
-    if (is_bf16) attn_prefill_kernel<bf16><<<g, 64, 0, s>>>(a);
-    else attn_prefill_kernel<float><<<g, 64, 0, s>>>(a);
+    if (is_bf16 && a.head_dim <= 128) {
+      dim3 g((a.S + 63) / 64, a.n_head, a.B);
+      const int hdp = (a.head_dim + 31) / 32 * 32;
+      if (hdp <= 64) attn_prefill_mfma_kernel<64><<<g, 256, 0, s>>>(a);
+      else if (hdp <= 96) attn_prefill_mfma_kernel<96><<<g, 256, 0, s>>>(a);
+      else attn_prefill_mfma_kernel<128><<<g, 256, 0, s>>>(a);
+    } else {
+      dim3 g(a.S, a.n_head, a.B);
+      if (is_bf16) attn_prefill_kernel<bf16><<<g, 64, 0, s>>>(a);
+      else attn_prefill_kernel<float><<<g, 64, 0, s>>>(a);
+    }
   }
 }
 

@@ -89,7 +89,7 @@ struct bs_stage {
   float* xa = nullptr;   // fp32 [T][h]
   float* xb = nullptr;   // fp32 [T][h]
   float* attn = nullptr; // fp32 [T][h]
-  float* q = nullptr;    // fp32 [T][h]
+  void* q = nullptr;     // act [T][h]
   void* xn = nullptr;    // act [T][h]
   void* ctx = nullptr;   // act [T][h]
   void* g = nullptr;     // act [T][4h]
@@ -346,7 +346,7 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   s->xa = (float*)(s->ws + wo[wi++]);
   s->xb = (float*)(s->ws + wo[wi++]);
   s->attn = (float*)(s->ws + wo[wi++]);
-  s->q = (float*)(s->ws + wo[wi++]);
+  s->q = s->ws + wo[wi++];
   s->xn = s->ws + wo[wi++];
   s->ctx = s->ws + wo[wi++];
   s->g = s->ws + wo[wi++];

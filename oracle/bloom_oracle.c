@@ -26,7 +26,7 @@
  * [slot, slot+B) hold positions [0, past_len) on entry; S new positions are appended.
  *
  * bf16 mode emulates the device path's storage roundings exactly (weights, LN outputs
- * feeding GEMMs, K/V cache, attention context, GELU output) while accumulating in fp32,
+ * feeding GEMMs, q, K/V cache, attention context, GELU output) while accumulating in fp32,
  * so GPU-vs-oracle differences are accumulation-order only.
  *
  * Parity pinning: checked against transformers' BloomForCausalLM on CPU fp32 with the
@@ -256,7 +256,9 @@ int or_forward(or_stage *s, int B, int S, int slot, int past_len, const void *in
         float *sc = (float *)malloc(sizeof(float) * nk_max);
         for (int t = 0; t < S; t++) {
           int m = b * S + t, nk = past_len + t + 1; /* causal: keys 0..pos */
-          const float *q = qkv + (size_t)m * 3 * h + (size_t)hh * 3 * hd;
+          const float *q0 = qkv + (size_t)m * 3 * h + (size_t)hh * 3 * hd;
+          float q[256];  /* the device stores q in the activation dtype (bf16 mode: rounded) */
+          for (int d = 0; d < hd; d++) q[d] = rb(s, q0[d]);
           float mx = -INFINITY;
           for (int j = 0; j < nk; j++) {
             float qk = dotf(q, kv_ptr(s, li, 0, slot + b, hh, j), hd);
