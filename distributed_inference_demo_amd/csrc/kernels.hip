@@ -820,12 +820,12 @@ static int gemv_waves(int N, int K) {
   return waves;
 }
 
-template <int R, int MM, bool LN>
+template <int R, int MM, bool LN, int U = 2>
 static void gemv_rows_launch(const bf16* X, const LnArgs& ln, const bf16* W, int M, int N, int K, const Epi& ep,
                              hipStream_t s) {
   const size_t shm = 256 + (LN ? (size_t)M * K * sizeof(bf16) : 0);
   const int blocks = (N + 4 * R - 1) / (4 * R);
-  gemv_rows_kernel<R, MM, 2, LN><<<blocks, 256, shm, s>>>(W, X, ln, M, N, K, ep);
+  gemv_rows_kernel<R, MM, U, LN><<<blocks, 256, shm, s>>>(W, X, ln, M, N, K, ep);
 }
 
 template <bool LN>
@@ -835,16 +835,31 @@ static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, i
   // M = 3..4: rows loses to the MFMA GEMV on LN-fused and large shapes
   // (tools/gemv_bench.hip, profiles/r01_gemv_bench_m4.log); keep it for small plain GEMVs and the head.
   if (M > 2 && ep.kind != EPI_ARGMAX && (LN || (size_t)N * K > (size_t)16 << 20)) return false;
+  // Tile choice from tools/gemv_bench.hip (profiles/r01_gemv_bench_m1_ur.log): U = 4 chunks of
+  // every row in flight; the LN variants take 2-4 rows per wave on wide N to amortise the
+  // per-block LayerNorm prologue; the head (argmax, 16 rows per block) keeps U = 2 on long K.
   if (ep.kind == EPI_ARGMAX) {  // a block = one 16-column tile
-    if (M == 1) gemv_rows_launch<4, 1, LN>(x, ln, w, M, N, K, ep, s);
-    else if (M == 2) gemv_rows_launch<4, 2, LN>(x, ln, w, M, N, K, ep, s);
-    else gemv_rows_launch<4, 4, LN>(x, ln, w, M, N, K, ep, s);
+    if (K <= 2048) {
+      if (M == 1) gemv_rows_launch<4, 1, LN, 4>(x, ln, w, M, N, K, ep, s);
+      else if (M == 2) gemv_rows_launch<4, 2, LN, 4>(x, ln, w, M, N, K, ep, s);
+      else gemv_rows_launch<4, 4, LN, 4>(x, ln, w, M, N, K, ep, s);
+    } else {
+      if (M == 1) gemv_rows_launch<4, 1, LN, 2>(x, ln, w, M, N, K, ep, s);
+      else if (M == 2) gemv_rows_launch<4, 2, LN, 2>(x, ln, w, M, N, K, ep, s);
+      else gemv_rows_launch<4, 4, LN, 2>(x, ln, w, M, N, K, ep, s);
+    }
     return true;
   }
-  const bool wide = N >= 8192;  // many rows: 2 rows per wave amortise the x reads and the LN prologue
-  if (M == 1) { if (wide) gemv_rows_launch<2, 1, LN>(x, ln, w, M, N, K, ep, s); else gemv_rows_launch<1, 1, LN>(x, ln, w, M, N, K, ep, s); }
-  else if (M == 2) { if (wide) gemv_rows_launch<2, 2, LN>(x, ln, w, M, N, K, ep, s); else gemv_rows_launch<1, 2, LN>(x, ln, w, M, N, K, ep, s); }
-  else { if (wide) gemv_rows_launch<2, 4, LN>(x, ln, w, M, N, K, ep, s); else gemv_rows_launch<1, 4, LN>(x, ln, w, M, N, K, ep, s); }
+  const int R = !LN ? 1 : (N >= 12288 ? 4 : (N >= 6144 ? 2 : 1));
+  auto go = [&](auto rc) {
+    constexpr int RR = decltype(rc)::value;
+    if (M == 1) gemv_rows_launch<RR, 1, LN, 4>(x, ln, w, M, N, K, ep, s);
+    else if (M == 2) gemv_rows_launch<RR, 2, LN, 4>(x, ln, w, M, N, K, ep, s);
+    else gemv_rows_launch<RR, 4, LN, 4>(x, ln, w, M, N, K, ep, s);
+  };
+  if (R == 1) go(EpiKindC<1>{});
+  else if (R == 2) go(EpiKindC<2>{});
+  else go(EpiKindC<4>{});
   return true;
 }
 
