@@ -37,10 +37,12 @@ def parse():
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     p.add_argument("--no-head-split", action="store_true", help="pipeline: keep the whole lm_head on the last stage")
+    p.add_argument("--engine", default="auto", choices=["auto", "launches", "persistent"],
+                   help="decode engine (bs_set_engine): auto = one persistent launch per step when eligible")
     return p.parse_args()
 
 
-def pmc_traffic(args, timeout=240):
+def pmc_traffic(args, kernel_tag, timeout=240):
     """roofline.traffic: HBM bytes per decode-GEMV launch from two separate rocprofv3 --pmc passes
     (FETCH_SIZE, then WRITE_SIZE) over a short child run of this same workload.  gfx950 correction
     (MI355X_MICROARCH.md section HBM): FETCH_SIZE counts half the bytes of wide coalesced reads ->
@@ -58,7 +60,7 @@ def pmc_traffic(args, timeout=240):
         cmd = [prof, "--pmc", counter, "-d", out, "-o", counter.lower(), "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--steps", "8", "--warmup", "2", "--cpu-baseline", "0",
                "--no-profile", "--no-pmc", "--model", args.model, "--batch", str(args.batch), "--prompt",
-               str(args.prompt), "--dtype", args.dtype, "--seed", str(args.seed)]
+               str(args.prompt), "--dtype", args.dtype, "--seed", str(args.seed), "--engine", args.engine]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
         except subprocess.TimeoutExpired:
@@ -69,10 +71,10 @@ def pmc_traffic(args, timeout=240):
             return None, f"rocprofv3 {counter} pass failed (rc {r.returncode})"
         vals = []
         for row in csv.DictReader(open(files[0])):
-            if row["Counter_Name"] == counter and "gemv" in row["Kernel_Name"]:
+            if row["Counter_Name"] == counter and kernel_tag in row["Kernel_Name"]:
                 vals.append(float(row["Counter_Value"]))
         if not vals:
-            return None, f"no gemv dispatches in the {counter} pass"
+            return None, f"no {kernel_tag} dispatches in the {counter} pass"
         vals = vals[len(vals) // 4:]  # drop the prefill/warm-up quarter
         scale = 2 * 1024 if counter == "FETCH_SIZE" else 1024
         tot[counter] = (sum(vals) / len(vals) * scale, len(vals))
@@ -129,6 +131,8 @@ def bench_single(args):
     st = Stage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, m.n_layer, dtype=args.dtype, device=0, max_batch=B,
                max_ctx=max_ctx, max_tokens=max(B * P, B), seed=args.seed)
     wbytes = st.info()["weight_bytes"]
+    st.set_engine(args.engine)
+    engine = st.engine(B)
     cs = torch.cuda.Stream()  # a real stream (the legacy default stream cannot be graph-captured)
     with torch.cuda.stream(cs):
         stream = cs.cuda_stream
@@ -154,10 +158,11 @@ def bench_single(args):
             past += 1
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        # roofline pass: the same decode steps, eager, HIP events around every weight GEMV
+        # roofline pass: the same decode steps, HIP events around the dominant kernel: the whole
+        # persistent step (class 4) or, on the launch engine, every weight GEMV (class 1, eager)
         g_ms = g_n = g_bytes = 0
         if prof_steps:
-            st.profile_enable(1)
+            st.profile_enable(4 if engine == "persistent" else 1)
             for _ in range(prof_steps):
                 st.forward(tok, tok, B, 1, slot=0, past_len=past, stream=stream)
                 past += 1
@@ -177,21 +182,28 @@ def bench_single(args):
         "config": {"workload": f"{m.name} single stage on 1 MI355X, batch {B} decode after a {P}-token prefill "
                                "(BASELINE.json configs[1])",
                    "model": m.name, "stages": 1, "layers_per_stage": [m.n_layer], "batch": B, "prompt": P,
-                   "ctx_range": [P + W, P + W + K], "parallelism": "pp1", "weight_bytes": wbytes},
+                   "ctx_range": [P + W, P + W + K], "parallelism": "pp1", "weight_bytes": wbytes,
+                   "engine": engine},
     }
     if g_n:
         avg_ms = g_ms / g_n
         ach = (g_bytes / g_n) / (avg_ms * 1e-3) / 1e9
-        traffic, note = (None, "--no-pmc") if args.no_pmc else pmc_traffic(args)
-        res["roofline"] = {"bound": "hbm", "kernel": "gemv_rows_kernel (every decode weight GEMV: LN+QKV, dense, "
-                                                    "LN+fc1, fc2, ln_f+lm_head)",
+        if engine == "persistent":
+            tag, kname = "decode_engine", ("decode_engine_kernel: the whole decode step in one launch (all layers' "
+                                           "LN/QKV/attention/dense/fc1/fc2 + ln_f/lm_head/argmax)")
+            unit_note = "algorithmic bytes per launch = the step's weights + K/V read and append + hidden in/out"
+        else:
+            tag, kname = "gemv", "gemv_rows_kernel (every decode weight GEMV: LN+QKV, dense, LN+fc1, fc2, ln_f+lm_head)"
+            unit_note = "algorithmic bytes per launch = weights + bias + activations of the GEMV"
+        traffic, note = (None, "--no-pmc") if args.no_pmc else pmc_traffic(args, tag)
+        res["roofline"] = {"bound": "hbm", "kernel": kname,
                            "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
                            "traffic": traffic, "launches": g_n, "avg_us": avg_ms * 1e3,
-                           "algo_bytes_per_launch": g_bytes / g_n,
+                           "algo_bytes_per_launch": g_bytes / g_n, "algo_note": unit_note,
                            "traffic_note": ("HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), "
                                             "separate rocprofv3 --pmc passes, gfx950 x2 fetch correction; "
                                             f"{note} launches" if traffic else f"traffic unavailable: {note}"),
-                           "measured": f"HIP events on the stage stream around each GEMV launch, {prof_steps} eager "
+                           "measured": f"HIP events on the stage stream around each launch, {prof_steps} "
                                        "decode steps right after the timed region"}
     res["stage_hbm"] = {"algo_bytes_per_step": step_bytes, "achieved_GBps": step_bytes / (ms_step * 1e-3) / 1e9,
                         "frac_of_peak": step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS}

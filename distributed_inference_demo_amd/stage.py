@@ -78,14 +78,21 @@ EXPORTS = [
     "bs_init_stage", "bs_forward", "bs_reset_kv", "bs_release", "bs_last_error", "bs_stage_info",
     "bs_stage_weight_count", "bs_abi_version", "bs_profile_enable", "bs_profile_read",
     "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
-    "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice",
+    "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice", "bs_set_engine", "bs_get_engine",
+    "bs_engine_status", "bs_engine_trace",
 ]
+
+ENGINE_AUTO, ENGINE_LAUNCHES, ENGINE_PERSISTENT = 0, 1, 2
 
 _LIB = None
 
 
 def lib():
-    """Load the HIP library.  There is no CPU fallback: a missing library is an error."""
+    """Load the HIP library.  There is no CPU fallback: a missing library is an error.
+
+    A process that also uses PyTorch must import torch before the first call: torch ships its own
+    libamdhip64.so.7, and the copy loaded first serves the whole process (torch fails to find the
+    device on the system ROCm copy)."""
     global _LIB
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
@@ -116,6 +123,10 @@ def lib():
         L.bs_read_weights.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, vp]
         L.bs_head_norm.argtypes = [vp, vp, i32, i32, vp, vp]
         L.bs_head_slice.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+        L.bs_set_engine.argtypes = [vp, i32]
+        L.bs_get_engine.argtypes = [vp, i32]
+        L.bs_engine_status.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
+        L.bs_engine_trace.argtypes = [vp, vp, ctypes.c_uint64, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         _LIB = L
     return _LIB
 
@@ -180,6 +191,32 @@ class Stage:
         for r in range(slot, slot + batch):
             self.past[r] = past + seq
         return out
+
+    # ---- decode engine selection (bs_set_engine): "auto", "launches" or "persistent"
+    def set_engine(self, mode):
+        m = {"auto": ENGINE_AUTO, "launches": ENGINE_LAUNCHES, "persistent": ENGINE_PERSISTENT}.get(mode, mode)
+        _check(lib().bs_set_engine(self._h, int(m)))
+
+    def engine(self, batch=1):
+        """Engine a decode step of `batch` rows runs on: "persistent" or "launches"."""
+        rc = lib().bs_get_engine(self._h, batch)
+        if rc < 0:
+            _check(rc)
+        return "persistent" if rc == ENGINE_PERSISTENT else "launches"
+
+    def engine_trace(self):
+        """Phase stamps of the last persistent launch, uint64 [workgroups][stride] (BS_ENGINE_TRACE=1)."""
+        n, st = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib().bs_engine_trace(self._h, None, 0, ctypes.byref(n), ctypes.byref(st)))
+        out = np.empty((n.value, st.value), np.uint64)
+        _check(lib().bs_engine_trace(self._h, out.ctypes.data, out.size, ctypes.byref(n), ctypes.byref(st)))
+        return out
+
+    def engine_status(self):
+        """Give-up codes of persistent launches since the last call (0 = all launches completed)."""
+        code = ctypes.c_uint32(0)
+        _check(lib().bs_engine_status(self._h, ctypes.byref(code)))
+        return code.value
 
     # ---- vocabulary-parallel head (device pointers, stream ordered)
     def head_norm(self, hidden, batch, seq, xn, stream=None):

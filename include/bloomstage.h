@@ -124,6 +124,29 @@ int bs_head_norm(bs_stage *stage, const float *hidden, int32_t batch, int32_t se
 int bs_head_slice(bs_stage *stage, const void *xn, int32_t batch, const uint64_t *keys_in, uint64_t *keys_out,
                   int32_t *tokens, void *stream);
 
+/* ---- Decode engine (S = 1 steps of B <= 4 rows on bf16 stages with hidden % 512 == 0) ----
+ * BS_ENGINE_PERSISTENT: the whole stage step is ONE kernel launch, a workgroup per CU walking
+ *   every layer (weights of the next op requested before waiting on the current one; in-launch
+ *   hand-offs).  BS_ENGINE_LAUNCHES: one kernel per op, captured in a
+ *   hipGraph.  BS_ENGINE_AUTO (default) is the launch engine unless BS_DECODE_ENGINE=persistent is
+ *   set in the environment; the persistent engine runs only on eligible steps.
+ * No reference counterpart: the reference has one engine (ORT Session::Run, inference.cpp:207-215). */
+#define BS_ENGINE_AUTO 0
+#define BS_ENGINE_LAUNCHES 1
+#define BS_ENGINE_PERSISTENT 2
+int bs_set_engine(bs_stage *stage, int32_t mode);
+/* Engine a decode step of `batch` rows would run on (BS_ENGINE_LAUNCHES or BS_ENGINE_PERSISTENT). */
+int bs_get_engine(const bs_stage *stage, int32_t batch);
+/* Give-up codes of persistent launches since the last call (0 = none).  A launch whose in-launch
+ * wait exceeded 200 ms aborts: its outputs are invalid, the next launch starts clean.  Host-I/O
+ * steps report this themselves as BS_ERR_DEVICE.  Synchronizes the stage's own stream. */
+int bs_engine_status(bs_stage *stage, uint32_t *code);
+/* Diagnostics: with BS_ENGINE_TRACE=1 in the environment at bs_init_stage, every persistent launch
+ * stores one 100 MHz s_memrealtime stamp per workgroup at each phase boundary; this copies the last
+ * launch's stamps ([n_wg][stride] uint64; index 0 = start, 1 + 12*layer + k, then the head).
+ * out = NULL: only report n_wg and stride.  Synchronizes the stage's own stream. */
+int bs_engine_trace(bs_stage *stage, uint64_t *out, uint64_t cap, int32_t *n_wg, int32_t *stride);
+
 /* Forget the cached positions of one KV row (slot), or of all rows when slot < 0. */
 int bs_reset_kv(bs_stage *stage, int32_t slot);
 
@@ -148,7 +171,8 @@ int bs_read_weights(const bs_stage *stage, uint64_t offset, uint64_t count, floa
 int bs_prompt_ids(uint64_t seed, int32_t n, int32_t vocab, int32_t *out);
 
 /* Profiling: time every launch of one kernel class with HIP events on the stage stream.
- * kernel_class: 0 off, 1 weight GEMV (decode), 2 GEMM (prefill), 3 attention.
+ * kernel_class: 0 off, 1 weight GEMV (decode), 2 GEMM (prefill), 3 attention,
+ *   4 persistent decode step (one launch per step; bytes = the step's algorithmic HBM bytes).
  * bs_profile_read returns accumulated milliseconds, launch count and algorithmic bytes
  * (or flops for class 2) since the last bs_profile_enable; it synchronizes the stream. */
 int bs_profile_enable(bs_stage *stage, int32_t kernel_class);

@@ -3,6 +3,12 @@ import sys
 
 import pytest
 
+# One HIP runtime per process: PyTorch ships its own libamdhip64.so.7 and whichever copy loads first
+# serves both it and libbloomstage.so.  Loaded after the system ROCm 7.2 copy (i.e. after the first
+# Stage), torch's device detection fails ("no ROCm-capable device"), so torch goes first, as it does
+# in bench.py and the pipeline driver.
+import torch  # noqa: F401,E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
