@@ -65,10 +65,11 @@ struct AttnArgs {
   int past;
   int n_head, head_dim, max_ctx, hidden;
   float inv_norm;
-  float* part_acc;     // workspace [B][n_head][max_chunks][head_dim]
-  float* part_ml;      // workspace [B][n_head][max_chunks][2]
+  float* part_acc;     // workspace [max_batch][n_head][max_chunks][head_dim] (row = slot + b)
+  float* part_ml;      // workspace [max_batch][n_head][max_chunks][2]
   int max_chunks;
   int chunk;           // positions per chunk (decode) = 64
+  unsigned* tickets;   // [max_batch][n_head] split-merge tickets (zero between launches)
 };
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s);
 size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, int* max_chunks, int* chunk);

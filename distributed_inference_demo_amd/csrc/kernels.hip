@@ -401,22 +401,37 @@ __device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float ac
 
 // LayerNorm of M <= MM <= 4 rows (K <= 4096) into LDS as bf16, 256 threads, nn.LayerNorm
 // semantics.  Each thread keeps its <= 16 values per row in registers: one global pass, two
-// block reductions (mean, then the exact centred variance), normalise from registers.
+// block reductions (mean, then the exact centred variance), normalise from registers.  Split in
+// two so a kernel can put its own loads (the weight stream) between the row loads and the math.
 template <int MM>
-__device__ __forceinline__ void ln_rows_to_lds(const LnArgs& ln, int M, int K, bf16* xs, float* scratch) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float4 xv[MM][4];
-  float part[MM];
+__device__ __forceinline__ void ln_rows_load(const LnArgs& ln, int M, int K, float4 (&xv)[MM][4], uint2 (&gb)[4][2]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {  // gamma/beta with the rows: no round trip after the reductions
+    const int k = threadIdx.x * 4 + i * 1024;
+    gb[i][0] = k < K ? *reinterpret_cast<const uint2*>(ln.gamma + k) : make_uint2(0u, 0u);
+    gb[i][1] = k < K ? *reinterpret_cast<const uint2*>(ln.beta + k) : make_uint2(0u, 0u);
+  }
 #pragma unroll
   for (int m = 0; m < MM; m++) {
     const float* xr = ln.x + ((size_t)min(m, M - 1) * ln.row_stride + ln.row_offset) * K;
-    float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const int k = threadIdx.x * 4 + i * 1024;
       xv[m][i] = k < K ? *reinterpret_cast<const float4*>(xr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-      acc += (xv[m][i].x + xv[m][i].y) + (xv[m][i].z + xv[m][i].w);
     }
+  }
+}
+
+template <int MM>
+__device__ __forceinline__ void ln_rows_finish(const LnArgs& ln, int M, int K, float4 (&xv)[MM][4],
+                                               const uint2 (&gb)[4][2], bf16* xs, float* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float part[MM];
+#pragma unroll
+  for (int m = 0; m < MM; m++) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; i++) acc += (xv[m][i].x + xv[m][i].y) + (xv[m][i].z + xv[m][i].w);
     part[m] = wave_sum(acc);
   }
   if (lane == 0) {
@@ -455,8 +470,7 @@ __device__ __forceinline__ void ln_rows_to_lds(const LnArgs& ln, int M, int K, b
   for (int i = 0; i < 4; i++) {
     const int k = threadIdx.x * 4 + i * 1024;
     if (k < K) {
-      const uint2 graw = *reinterpret_cast<const uint2*>(ln.gamma + k);
-      const uint2 braw = *reinterpret_cast<const uint2*>(ln.beta + k);
+      const uint2 graw = gb[i][0], braw = gb[i][1];
       const float g[4] = {__uint_as_float(graw.x << 16), __uint_as_float(graw.x & 0xFFFF0000u),
                           __uint_as_float(graw.y << 16), __uint_as_float(graw.y & 0xFFFF0000u)};
       const float bb[4] = {__uint_as_float(braw.x << 16), __uint_as_float(braw.x & 0xFFFF0000u),
@@ -488,8 +502,12 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
   const bf16* wr[R];
 #pragma unroll
   for (int r = 0; r < R; r++) wr[r] = W + (size_t)min(n0 + r, N - 1) * K;
-  // the first U chunks of every row are requested before the (LN) prologue, so the weight
-  // stream is already in flight while the block normalises its activations
+  // LN variant: the activation rows are requested first, then the first U chunks of every
+  // weight row, then the LayerNorm math runs on the rows (their loads are the oldest, so waiting
+  // for them does not wait for the weights) while the weight stream is in flight
+  float4 xv[LN ? MM : 1][4];
+  uint2 gb[4][2];
+  if constexpr (LN) ln_rows_load<MM>(ln, M, K, xv, gb);
   bf16x8 wv[U][R];
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -500,7 +518,7 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
   const bf16* xg;
   int xstride;
   if constexpr (LN) {
-    ln_rows_to_lds<MM>(ln, M, K, xs, scratch);
+    ln_rows_finish<MM>(ln, M, K, xv, gb, xs, scratch);
     xg = xs; xstride = K;
   } else {
     xg = X; xstride = K;
@@ -851,15 +869,32 @@ static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, i
     return true;
   }
   const int R = !LN ? 1 : (N >= 12288 ? 4 : (N >= 6144 ? 2 : 1));
-  auto go = [&](auto rc) {
-    constexpr int RR = decltype(rc)::value;
-    if (M == 1) gemv_rows_launch<RR, 1, LN, 4>(x, ln, w, M, N, K, ep, s);
-    else if (M == 2) gemv_rows_launch<RR, 2, LN, 4>(x, ln, w, M, N, K, ep, s);
-    else gemv_rows_launch<RR, 4, LN, 4>(x, ln, w, M, N, K, ep, s);
+  // U = 512-element chunks of a row in flight per iteration: an exact divisor of the row's chunk
+  // count, so every row streams in whole rounds with no re-loaded tail (K = 1536 -> 3, 6144 -> 12,
+  // 4096 -> 8, 16384 -> 8, 2560 -> 5, 1024 -> 2); fallback 4.
+  const int cpr = K / 512;
+  const int U = (K % 512) ? 4 : (cpr <= 3 || cpr == 5 || cpr == 8 || cpr == 12) ? cpr
+              : (cpr % 12 == 0 ? 12 : (cpr % 8 == 0 ? 8 : (cpr % 5 == 0 ? 5 : 4)));
+  auto go = [&](auto rc, auto uc) {
+    constexpr int RR = decltype(rc)::value, UU = decltype(uc)::value;
+    if (M == 1) gemv_rows_launch<RR, 1, LN, UU>(x, ln, w, M, N, K, ep, s);
+    else if (M == 2) gemv_rows_launch<RR, 2, LN, UU>(x, ln, w, M, N, K, ep, s);
+    else gemv_rows_launch<RR, 4, LN, UU>(x, ln, w, M, N, K, ep, s);
   };
-  if (R == 1) go(EpiKindC<1>{});
-  else if (R == 2) go(EpiKindC<2>{});
-  else go(EpiKindC<4>{});
+  auto gu = [&](auto rc) {
+    switch (U) {
+      case 1: go(rc, EpiKindC<1>{}); break;
+      case 2: go(rc, EpiKindC<2>{}); break;
+      case 3: go(rc, EpiKindC<3>{}); break;
+      case 5: go(rc, EpiKindC<5>{}); break;
+      case 8: go(rc, EpiKindC<8>{}); break;
+      case 12: go(rc, EpiKindC<12>{}); break;
+      default: go(rc, EpiKindC<4>{}); break;
+    }
+  };
+  if (R == 1) gu(EpiKindC<1>{});
+  else if (R == 2) gu(EpiKindC<2>{});
+  else gu(EpiKindC<4>{});
   return true;
 }
 
@@ -930,42 +965,39 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
 // ------------------------------------------------------------------------------------
 // Decode (S == 1).  Block (head, row b, split) of WV waves; wave w of split sp takes the 64-position
 // chunks c = w + WV*(sp + nsplit*j).  16 lanes cover one 8-dim slice each of a key/value row, so
-// every load instruction reads 4 whole rows (coalesced); a chunk's V rows are loaded together with
-// its K rows, before the softmax.  Scores = ALiBi + q.k/sqrt(hd); online softmax across the wave's
-// chunks; the wave partials merge through LDS.  nsplit == 1: the block writes ctx; otherwise it
-// writes a (max, sum, context) partial that attn_merge_kernel combines (small B*heads: spreads the
-// KV stream of one (row, head) over several CUs).  No global atomics or fences.
+// every load instruction reads 4 whole rows (coalesced); a chunk's K and V rows are requested
+// before q is staged (they do not depend on it), so the first chunk's HBM round trip overlaps the
+// q load.  Scores = ALiBi + q.k/sqrt(hd); online softmax across the wave's chunks; the wave
+// partials merge through LDS.  nsplit == 1: the block writes ctx.  Otherwise it publishes a
+// (max, sum, context) partial write-through (sc1) and takes a ticket; the block drawing the last
+// ticket of its (row, head) merges all partials (sc1 loads, issued together) and writes ctx —
+// MI355X_MICROARCH.md "Valid forms" row 1 (counter form, the last adder reads).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)0xFFFFFFFF, 0x00020000);
+}
+
 template <typename T, int WV>
 __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float qs[128];
   __shared__ float es[WV][64];
   __shared__ float pm[WV], pl[WV];
   __shared__ float pacc[WV][128];
+  __shared__ int last;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int head = blockIdx.x, b = blockIdx.y, sp = blockIdx.z, nsplit = gridDim.z;
   const int hd = a.head_dim;
-  for (int d = threadIdx.x; d < hd; d += WV * 64) qs[d] = to_f32(((const T*)a.q)[(size_t)b * a.hidden + head * hd + d]);
-  __syncthreads();
   const int past = a.past_dev ? *a.past_dev : a.past;
   const int nk = past + 1, nlast = nk - 1;
   const int nch = (nk + 63) >> 6;
   const size_t rowbase = ((size_t)(a.slot + b) * a.n_head + head) * a.max_ctx;
   const T* kb = (const T*)a.k_cache + rowbase * hd;
   const T* vb = (const T*)a.v_cache + rowbase * hd;
-  const float slope = a.slopes[head];
   const int grp = lane >> 4, dl = lane & 15;
   const bool dval = dl * 8 < hd;
   const int doff = dval ? dl * 8 : 0;  // masked lanes re-read dims 0..7 (harmless)
-  float qv[8];
-  {
-    const float4 q0 = *reinterpret_cast<const float4*>(&qs[doff]);
-    const float4 q1 = *reinterpret_cast<const float4*>(&qs[doff + 4]);
-    qv[0] = q0.x; qv[1] = q0.y; qv[2] = q0.z; qv[3] = q0.w; qv[4] = q1.x; qv[5] = q1.y; qv[6] = q1.z; qv[7] = q1.w;
-  }
-  float m_run = -INFINITY, l_run = 0.f;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int c = w + WV * sp; c < nch; c += WV * nsplit) {
-    typename Raw8<T>::type kr[16], vr[16];
+  typedef typename Raw8<T>::type R8;
+  R8 kr[16], vr[16];
+  auto load_chunk = [&](int c) {
 #pragma unroll
     for (int it = 0; it < 16; it++) {
       const int pr = min(c * 64 + it * 4 + grp, nlast);
@@ -976,6 +1008,22 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
       const int pr = min(c * 64 + it * 4 + grp, nlast);
       raw_load(vb + (size_t)pr * hd + doff, vr[it]);
     }
+  };
+  int c = w + WV * sp;
+  if (c < nch) load_chunk(c);  // first chunk in flight before q
+  for (int d = threadIdx.x; d < hd; d += WV * 64) qs[d] = to_f32(((const T*)a.q)[(size_t)b * a.hidden + head * hd + d]);
+  __syncthreads();
+  const float slope = a.slopes[head];
+  float qv[8];
+  {
+    const float4 q0 = *reinterpret_cast<const float4*>(&qs[doff]);
+    const float4 q1 = *reinterpret_cast<const float4*>(&qs[doff + 4]);
+    qv[0] = q0.x; qv[1] = q0.y; qv[2] = q0.z; qv[3] = q0.w; qv[4] = q1.x; qv[5] = q1.y; qv[6] = q1.z; qv[7] = q1.w;
+  }
+  float m_run = -INFINITY, l_run = 0.f;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (; c < nch; c += WV * nsplit) {
+    if (c != w + WV * sp) load_chunk(c);
     float sc[16];
 #pragma unroll
     for (int it = 0; it < 16; it++) {
@@ -1026,11 +1074,11 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   }
   if (lane == 0) { pm[w] = m_run; pl[w] = l_run; }
   __syncthreads();
+  float M = -INFINITY, L = 0.f, o = 0.f;
   if (threadIdx.x < hd) {
-    float M = pm[0];
+    M = pm[0];
 #pragma unroll
     for (int ww = 1; ww < WV; ww++) M = fmaxf(M, pm[ww]);
-    float L = 0.f, o = 0.f;
     if (M != -INFINITY) {  // a split past the context end holds no chunk
 #pragma unroll
       for (int ww = 0; ww < WV; ww++) {
@@ -1039,32 +1087,68 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
         o += wgt * pacc[ww][threadIdx.x];
       }
     }
-    if (nsplit == 1) {
-      ((T*)a.ctx_out)[(size_t)b * a.hidden + head * hd + threadIdx.x] = from_f32<T>(o / L);
-    } else {
-      const size_t pidx = ((size_t)b * a.n_head + head) * a.max_chunks + sp;
-      a.part_acc[pidx * hd + threadIdx.x] = o;
-      if (threadIdx.x == 0) { a.part_ml[pidx * 2] = M; a.part_ml[pidx * 2 + 1] = L; }
+  }
+  T* ctx = (T*)a.ctx_out + (size_t)b * a.hidden + head * hd;
+  if (nsplit == 1) {
+    if (threadIdx.x < hd) ctx[threadIdx.x] = from_f32<T>(o / L);
+    return;
+  }
+  // ---- split partial (sc1 write-through), ticket, last arriver merges
+  const size_t pair = (size_t)(a.slot + b) * a.n_head + head;
+  float* pacc_g = a.part_acc + pair * a.max_chunks * hd;  // [nsplit][hd]
+  float* pml_g = a.part_ml + pair * a.max_chunks * 2;     // [nsplit][2]
+  if (threadIdx.x < hd)
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), attn_rsrc(pacc_g), (uint32_t)(sp * hd + threadIdx.x) * 4, 0, 16);
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(M), attn_rsrc(pml_g), (uint32_t)sp * 8, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(L), attn_rsrc(pml_g), (uint32_t)sp * 8 + 4, 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    typedef __attribute__((address_space(1))) unsigned gu32;
+    const unsigned old = __hip_atomic_fetch_add((gu32*)(a.tickets + pair), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == (unsigned)(nsplit - 1);
+    if (last) __hip_atomic_store((gu32*)(a.tickets + pair), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  // one round trip: every thread takes all nsplit (m, l) pairs (same words in every lane) and its
+  // context column of every split, all loads in flight together
+  if (threadIdx.x < hd) {
+    float mx = -INFINITY;
+    float acc2 = 0.f, lsum = 0.f;
+    for (int t0 = 0; t0 < nsplit; t0 += 8) {
+      float m8[8], l8[8], o8[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int t = min(t0 + u, nsplit - 1);
+        m8[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(attn_rsrc(pml_g), (uint32_t)t * 8, 0, 16));
+        l8[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(attn_rsrc(pml_g), (uint32_t)t * 8 + 4, 0, 16));
+        o8[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(attn_rsrc(pacc_g), (uint32_t)(t * hd + threadIdx.x) * 4, 0, 16));
+      }
+      // online merge of this group of 8 (duplicates past nsplit masked out)
+      float gm = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < 8; u++) gm = t0 + u < nsplit ? fmaxf(gm, m8[u]) : gm;
+      const float nm = fmaxf(mx, gm);
+      if (nm != -INFINITY) {
+        const float sc = __expf(mx - nm);  // mx = -inf on the first group: 0
+        acc2 *= sc;
+        lsum *= sc;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          if (t0 + u < nsplit && m8[u] != -INFINITY) {
+            const float wgt = __expf(m8[u] - nm);
+            acc2 += wgt * o8[u];
+            lsum += wgt * l8[u];
+          }
+        }
+        mx = nm;
+      }
     }
+    ctx[threadIdx.x] = from_f32<T>(acc2 / lsum);
   }
-}
-
-// Merge the nsplit partials of each (row, head) into ctx.
-template <typename T>
-__global__ __launch_bounds__(128) void attn_merge_kernel(AttnArgs a, int nsplit) {
-  const int head = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
-  const size_t base = ((size_t)b * a.n_head + head) * a.max_chunks;
-  float M = -INFINITY;
-  for (int sp = 0; sp < nsplit; sp++) M = fmaxf(M, a.part_ml[(base + sp) * 2]);
-  float L = 0.f, o = 0.f;
-  for (int sp = 0; sp < nsplit; sp++) {
-    const float m = a.part_ml[(base + sp) * 2];
-    if (m == -INFINITY) continue;
-    const float wgt = __expf(m - M);
-    L += wgt * a.part_ml[(base + sp) * 2 + 1];
-    if (d < a.head_dim) o += wgt * a.part_acc[(base + sp) * a.head_dim + d];
-  }
-  if (d < a.head_dim) ((T*)a.ctx_out)[(size_t)b * a.hidden + head * a.head_dim + d] = from_f32<T>(o / L);
 }
 
 // S > 1: one wave per (query, head, row), online softmax over 64-key blocks.
@@ -1271,28 +1355,21 @@ size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, 
 
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
   if (a.S == 1) {
-    // One 8-wave block per (row, head) when that already fills the chip; otherwise 4-wave
-    // blocks split the context so ~256 blocks stream the KV cache, then a merge kernel.
-    // Measured (bloom-1b1, B = 1, ctx ~600): one block per (row, head) 9.2 us vs split + merge
-    // 6.6 + 4.6 us — a kernel costs ~4 us of fixed latency at this size, so split only when a
-    // single block would walk more than 2 chunks per wave (ctx > 1024).
+    // One 8-wave block per (row, head) when that already fills the chip; otherwise 4-wave blocks
+    // split the context so ~256 blocks stream the KV cache, and the last split of each (row, head)
+    // merges in the same launch (no merge kernel, no extra boundary).
     const int pairs = a.B * a.n_head;
-    if (pairs >= 192 || a.max_chunks <= 16) {
+    if (pairs >= 192 || a.max_chunks <= 4) {
       dim3 g(a.n_head, a.B, 1);
       if (is_bf16) attn_decode_kernel<bf16, 8><<<g, 512, 0, s>>>(a);
       else attn_decode_kernel<float, 8><<<g, 512, 0, s>>>(a);
     } else {
       int nsplit = (256 + pairs - 1) / pairs;
       nsplit = min(nsplit, (a.max_chunks + 3) / 4);
-      nsplit = max(nsplit, 1);
-      dim3 g(a.n_head, a.B, nsplit), gm(a.n_head, a.B);
-      if (is_bf16) {
-        attn_decode_kernel<bf16, 4><<<g, 256, 0, s>>>(a);
-        if (nsplit > 1) attn_merge_kernel<bf16><<<gm, 128, 0, s>>>(a, nsplit);
-      } else {
-        attn_decode_kernel<float, 4><<<g, 256, 0, s>>>(a);
-        if (nsplit > 1) attn_merge_kernel<float><<<gm, 128, 0, s>>>(a, nsplit);
-      }
+      nsplit = max(1, min(nsplit, 64));
+      dim3 g(a.n_head, a.B, nsplit);
+      if (is_bf16) attn_decode_kernel<bf16, 4><<<g, 256, 0, s>>>(a);
+      else attn_decode_kernel<float, 4><<<g, 256, 0, s>>>(a);
     }
   } else {
     if (is_bf16 && a.head_dim <= 128) {

@@ -102,6 +102,7 @@ struct bs_stage {
   int* tok = nullptr;                  // [max_batch]
   int* ids = nullptr;                  // [T] staging for host ids
   int* past_dev = nullptr;
+  unsigned* att_tickets = nullptr;     // [max_batch][n_head]
   ProfClass prof;
   std::vector<std::pair<void*, size_t>> order;  // canonical weight order (BS_WEIGHTS_HOST layout)
   std::vector<std::pair<GraphKey, hipGraphExec_t>> graphs;  // captured decode steps
@@ -498,6 +499,7 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   wadd((size_t)desc->max_batch * 4);
   wadd(T * 4);
   wadd(256);
+  wadd((size_t)desc->max_batch * desc->n_head * 4);  // attention split-merge tickets
   s->wsbytes = woff;
   if (hipMalloc(&s->ws, s->wsbytes) != hipSuccess) return cleanup(fail(BS_ERR_OOM, "workspace allocation failed"));
   int wi = 0;
@@ -515,6 +517,7 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   s->tok = (int*)(s->ws + wo[wi++]);
   s->ids = (int*)(s->ws + wo[wi++]);
   s->past_dev = (int*)(s->ws + wo[wi++]);
+  s->att_tickets = (unsigned*)(s->ws + wo[wi++]);
   HIP_TRY(hipMemsetAsync(s->ws, 0, s->wsbytes, s->own));
   std::vector<float> sl(desc->n_head);
   alibi_slopes(desc->n_head, sl.data());
@@ -738,7 +741,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     a.q = s->q; a.k_cache = kbase; a.v_cache = kbase + s->kv_half; a.ctx_out = s->ctx; a.slopes = s->slopes;
     a.B = B; a.S = S; a.slot = slot; a.past = past; a.past_dev = past_dev; a.n_head = nh; a.head_dim = hd;
     a.max_ctx = d.max_ctx; a.hidden = h; a.inv_norm = inv_norm; a.part_acc = s->part_acc; a.part_ml = s->part_ml;
-    a.max_chunks = s->max_chunks; a.chunk = s->chunk;
+    a.max_chunks = s->max_chunks; a.chunk = s->chunk; a.tickets = s->att_tickets;
     {
       ProfScope p(s, st, 3, (double)B * nh * (double)(past + S) * hd * 2 * s->esz);
       launch_attention(s->bf16, a, st);
