@@ -17,7 +17,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 SOURCES = ["kernels.hip", "decode_engine.hip", "stage.hip", "codec.cpp"]
-HEADERS = ["common.h", "kernels.h", "decode_engine.h"]
+HEADERS = ["common.h", "kernels.h", "decode_engine.h", "attn_merge.h"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-Wno-unused-result", "-Wno-unused-value", f"-I{os.path.join(ROOT, 'include')}"]
 

@@ -70,9 +70,23 @@ struct AttnArgs {
   int max_chunks;
   int chunk;           // positions per chunk (decode) = 64
   unsigned* tickets;   // [max_batch][n_head] split-merge tickets (zero between launches)
+  int defer_merge;     // decode split > 1: leave the partials for the consumer (launch_linear_parts)
 };
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s);
 size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, int* max_chunks, int* chunk);
+// Context splits per (row, head) of a decode attention launch (1 = the block writes ctx itself).
+int attention_decode_splits(int B, int n_head, int max_chunks);
+
+// Split-attention partials as the consumer reads them (attn_merge.h).
+struct AttnParts {
+  const float* acc;  // AttnArgs::part_acc
+  const float* ml;   // AttnArgs::part_ml
+  int nsplit, n_head, head_dim, max_chunks, slot;
+};
+// Can launch_linear_parts run M rows of a K-wide ctx split `nsplit` ways?
+bool linear_parts_supported(int M, int K, int head_dim, int nsplit);
+// Weight GEMV on ctx = merge(partials) (bf16): the dense projection after a deferred-merge attention.
+void launch_linear_parts(const AttnParts& p, const void* W, int M, int N, int K, const Epi& ep, hipStream_t s);
 
 // keys -> token ids
 // Reduce the per-tile keys of each row (and keys_in[m] if given) -> keys_out[m] / tokens[m] (either optional).

@@ -12,6 +12,7 @@
 //  for S > 1; both causal + ALiBi over the contiguous per-stage KV cache.
 #include "common.h"
 #include "kernels.h"
+#include "attn_merge.h"
 
 #include <cstdlib>
 
@@ -491,23 +492,40 @@ __device__ __forceinline__ void ln_rows_finish(const LnArgs& ln, int M, int K, f
   __syncthreads();
 }
 
-template <int R, int MM, int U, bool LN>
+// Activation prologue of gemv_rows_kernel: X read as given, LayerNorm of fp32 rows, or the merge
+// of split-attention partials (attn_merge.h); the last two stage bf16 rows in LDS.
+enum XMode : int { X_PLAIN = 0, X_LN = 1, X_PARTS = 2 };
+constexpr int kPartsPre = 2;  // 4-column groups per thread whose partial loads go out before the weights
+
+template <int R, int MM, int U, int XM>
 __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
-                                                        LnArgs ln, int M, int N, int K, Epi ep) {
+                                                        LnArgs ln, AttnParts pa, int M, int N, int K, Epi ep) {
+  constexpr bool LN = XM == X_LN;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* scratch = reinterpret_cast<float*>(smem);                  // 64 floats
-  bf16* xs = reinterpret_cast<bf16*>(smem + 256);                    // LN: [M][K]
+  bf16* xs = reinterpret_cast<bf16*>(smem + 256);                    // LN / PARTS: [M][K]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n0 = (blockIdx.x * 4 + w) * R;
   const bf16* wr[R];
 #pragma unroll
   for (int r = 0; r < R; r++) wr[r] = W + (size_t)min(n0 + r, N - 1) * K;
-  // LN variant: the activation rows are requested first, then the first U chunks of every
-  // weight row, then the LayerNorm math runs on the rows (their loads are the oldest, so waiting
+  // LN / PARTS: the activation loads are issued first, then the first U chunks of every weight
+  // row, then the prologue math runs on the activations (their loads are the oldest, so waiting
   // for them does not wait for the weights) while the weight stream is in flight
   float4 xv[LN ? MM : 1][4];
   uint2 gb[4][2];
   if constexpr (LN) ln_rows_load<MM>(ln, M, K, xv, gb);
+  const int kq = K >> 2, ngroups = M * kq;  // PARTS: 4-column groups of all rows
+  PartsRegs pr[XM == X_PARTS ? kPartsPre : 1];
+  auto pld1 = [](const float* p, size_t i) { return p[i]; };
+  auto pld4 = [](const float* p, size_t i) { return *reinterpret_cast<const float4*>(p + i); };
+  if constexpr (XM == X_PARTS) {
+#pragma unroll
+    for (int it = 0; it < kPartsPre; it++) {
+      const int g = min((int)threadIdx.x + it * 256, ngroups - 1);
+      attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, pr[it]);
+    }
+  }
   bf16x8 wv[U][R];
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -519,6 +537,28 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
   int xstride;
   if constexpr (LN) {
     ln_rows_finish<MM>(ln, M, K, xv, gb, xs, scratch);
+    xg = xs; xstride = K;
+  } else if constexpr (XM == X_PARTS) {
+    auto put = [&](int g, const PartsRegs& r) {
+      float o[4];
+      attn_parts_combine(pa.nsplit, r, o);
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[j] = (bf16)o[j];
+      *reinterpret_cast<bf16x4*>(xs + (size_t)(g / kq) * K + (g % kq) * 4) = v;
+    };
+#pragma unroll
+    for (int it = 0; it < kPartsPre; it++) {
+      const int g = threadIdx.x + it * 256;
+      if (g < ngroups) put(g, pr[it]);
+    }
+    for (int g = threadIdx.x + kPartsPre * 256; g < ngroups; g += 256) {  // wide rows: load as we go
+      PartsRegs r;
+      attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, r);
+      put(g, r);
+    }
+    __syncthreads();
     xg = xs; xstride = K;
   } else {
     xg = X; xstride = K;
@@ -838,33 +878,36 @@ static int gemv_waves(int N, int K) {
   return waves;
 }
 
-template <int R, int MM, bool LN, int U = 2>
-static void gemv_rows_launch(const bf16* X, const LnArgs& ln, const bf16* W, int M, int N, int K, const Epi& ep,
-                             hipStream_t s) {
-  const size_t shm = 256 + (LN ? (size_t)M * K * sizeof(bf16) : 0);
+template <int R, int MM, int XM, int U = 2>
+static void gemv_rows_launch(const bf16* X, const LnArgs& ln, const AttnParts& pa, const bf16* W, int M, int N,
+                             int K, const Epi& ep, hipStream_t s) {
+  const size_t shm = 256 + (XM != X_PLAIN ? (size_t)M * K * sizeof(bf16) : 0);
   const int blocks = (N + 4 * R - 1) / (4 * R);
-  gemv_rows_kernel<R, MM, U, LN><<<blocks, 256, shm, s>>>(W, X, ln, M, N, K, ep);
+  gemv_rows_kernel<R, MM, U, XM><<<blocks, 256, shm, s>>>(W, X, ln, pa, M, N, K, ep);
 }
 
-template <bool LN>
-static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, int M, int N, int K, const Epi& ep,
-                               hipStream_t s) {
-  if (M > 4 || (K % 8) != 0 || K < 8 || (LN && K > 4096)) return false;
+template <int XM>
+static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const AttnParts& pa, const bf16* w, int M, int N,
+                               int K, const Epi& ep, hipStream_t s) {
+  constexpr bool LN = XM == X_LN;
+  if (M > 4 || (K % 8) != 0 || K < 8 || (XM != X_PLAIN && K > 4096)) return false;
   // M = 3..4: rows loses to the MFMA GEMV on LN-fused and large shapes
-  // (tools/gemv_bench.hip, profiles/r01_gemv_bench_m4.log); keep it for small plain GEMVs and the head.
-  if (M > 2 && ep.kind != EPI_ARGMAX && (LN || (size_t)N * K > (size_t)16 << 20)) return false;
+  // (tools/gemv_bench.hip, profiles/r01_gemv_bench_m4.log); keep it for small plain GEMVs and the head
+  // (and for PARTS, which only this kernel implements).
+  if (XM == X_PLAIN && M > 2 && ep.kind != EPI_ARGMAX && (size_t)N * K > (size_t)16 << 20) return false;
+  if (XM == X_LN && M > 2 && ep.kind != EPI_ARGMAX) return false;
   // Tile choice from tools/gemv_bench.hip (profiles/r01_gemv_bench_m1_ur.log): U = 4 chunks of
   // every row in flight; the LN variants take 2-4 rows per wave on wide N to amortise the
   // per-block LayerNorm prologue; the head (argmax, 16 rows per block) keeps U = 2 on long K.
   if (ep.kind == EPI_ARGMAX) {  // a block = one 16-column tile
     if (K <= 2048) {
-      if (M == 1) gemv_rows_launch<4, 1, LN, 4>(x, ln, w, M, N, K, ep, s);
-      else if (M == 2) gemv_rows_launch<4, 2, LN, 4>(x, ln, w, M, N, K, ep, s);
-      else gemv_rows_launch<4, 4, LN, 4>(x, ln, w, M, N, K, ep, s);
+      if (M == 1) gemv_rows_launch<4, 1, XM, 4>(x, ln, pa, w, M, N, K, ep, s);
+      else if (M == 2) gemv_rows_launch<4, 2, XM, 4>(x, ln, pa, w, M, N, K, ep, s);
+      else gemv_rows_launch<4, 4, XM, 4>(x, ln, pa, w, M, N, K, ep, s);
     } else {
-      if (M == 1) gemv_rows_launch<4, 1, LN, 2>(x, ln, w, M, N, K, ep, s);
-      else if (M == 2) gemv_rows_launch<4, 2, LN, 2>(x, ln, w, M, N, K, ep, s);
-      else gemv_rows_launch<4, 4, LN, 2>(x, ln, w, M, N, K, ep, s);
+      if (M == 1) gemv_rows_launch<4, 1, XM, 2>(x, ln, pa, w, M, N, K, ep, s);
+      else if (M == 2) gemv_rows_launch<4, 2, XM, 2>(x, ln, pa, w, M, N, K, ep, s);
+      else gemv_rows_launch<4, 4, XM, 2>(x, ln, pa, w, M, N, K, ep, s);
     }
     return true;
   }
@@ -877,9 +920,9 @@ static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, i
               : (cpr % 12 == 0 ? 12 : (cpr % 8 == 0 ? 8 : (cpr % 5 == 0 ? 5 : 4)));
   auto go = [&](auto rc, auto uc) {
     constexpr int RR = decltype(rc)::value, UU = decltype(uc)::value;
-    if (M == 1) gemv_rows_launch<RR, 1, LN, UU>(x, ln, w, M, N, K, ep, s);
-    else if (M == 2) gemv_rows_launch<RR, 2, LN, UU>(x, ln, w, M, N, K, ep, s);
-    else gemv_rows_launch<RR, 4, LN, UU>(x, ln, w, M, N, K, ep, s);
+    if (M == 1) gemv_rows_launch<RR, 1, XM, UU>(x, ln, pa, w, M, N, K, ep, s);
+    else if (M == 2) gemv_rows_launch<RR, 2, XM, UU>(x, ln, pa, w, M, N, K, ep, s);
+    else gemv_rows_launch<RR, 4, XM, UU>(x, ln, pa, w, M, N, K, ep, s);
   };
   auto gu = [&](auto rc) {
     switch (U) {
@@ -901,7 +944,7 @@ static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, i
 template <bool LN>
 static void gemv_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, int M, int N, int K, const Epi& ep,
                           hipStream_t s) {
-  if (!gemv_rows_disabled() && gemv_rows_dispatch<LN>(x, ln, w, M, N, K, ep, s)) return;
+  if (!gemv_rows_disabled() && gemv_rows_dispatch<LN ? X_LN : X_PLAIN>(x, ln, AttnParts{}, w, M, N, K, ep, s)) return;
   const int waves = gemv_waves(N, K);
   const bool two = M > 16;
   if (waves == 4) { if (two) gemv_launch<4, 2, LN>(x, ln, w, M, N, K, ep, s); else gemv_launch<4, 1, LN>(x, ln, w, M, N, K, ep, s); }
@@ -922,6 +965,16 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
   }
   launch_layernorm(is_bf16, x, nullptr, row_stride, row_offset, gamma, beta, xn_scratch, 0, M, K, eps, s);
   launch_linear(is_bf16, xn_scratch, W, M, N, K, ep, s);
+}
+
+bool linear_parts_supported(int M, int K, int head_dim, int nsplit) {
+  return M >= 1 && M <= 4 && K % 8 == 0 && K >= 8 && K <= 4096 && head_dim % 4 == 0 && nsplit >= 2 &&
+         nsplit <= kPartsMaxSplit;
+}
+
+void launch_linear_parts(const AttnParts& p, const void* W, int M, int N, int K, const Epi& ep, hipStream_t s) {
+  if (M <= 0) return;
+  gemv_rows_dispatch<X_PARTS>(nullptr, LnArgs{}, p, (const bf16*)W, M, N, K, ep, s);
 }
 
 void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int K, const Epi& ep, hipStream_t s) {
@@ -986,9 +1039,6 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int head = blockIdx.x, b = blockIdx.y, sp = blockIdx.z, nsplit = gridDim.z;
   const int hd = a.head_dim;
-  const int past = a.past_dev ? *a.past_dev : a.past;
-  const int nk = past + 1, nlast = nk - 1;
-  const int nch = (nk + 63) >> 6;
   const size_t rowbase = ((size_t)(a.slot + b) * a.n_head + head) * a.max_ctx;
   const T* kb = (const T*)a.k_cache + rowbase * hd;
   const T* vb = (const T*)a.v_cache + rowbase * hd;
@@ -997,20 +1047,26 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   const int doff = dval ? dl * 8 : 0;  // masked lanes re-read dims 0..7 (harmless)
   typedef typename Raw8<T>::type R8;
   R8 kr[16], vr[16];
-  auto load_chunk = [&](int c) {
+  auto load_chunk = [&](int c, int lim) {
 #pragma unroll
     for (int it = 0; it < 16; it++) {
-      const int pr = min(c * 64 + it * 4 + grp, nlast);
+      const int pr = min(c * 64 + it * 4 + grp, lim);
       raw_load(kb + (size_t)pr * hd + doff, kr[it]);
     }
 #pragma unroll
     for (int it = 0; it < 16; it++) {
-      const int pr = min(c * 64 + it * 4 + grp, nlast);
+      const int pr = min(c * 64 + it * 4 + grp, lim);
       raw_load(vb + (size_t)pr * hd + doff, vr[it]);
     }
   };
+  // The first chunk is requested before past_len is known (clamped to the cache, not the context:
+  // positions past the context are masked to p = 0 below; the cache is zero-initialised and only
+  // ever holds finite values, so their V rows contribute 0 * finite) and before q is staged.
   int c = w + WV * sp;
-  if (c < nch) load_chunk(c);  // first chunk in flight before q
+  if (c < a.max_chunks) load_chunk(c, a.max_ctx - 1);
+  const int past = a.past_dev ? *a.past_dev : a.past;
+  const int nk = past + 1, nlast = nk - 1;
+  const int nch = (nk + 63) >> 6;
   for (int d = threadIdx.x; d < hd; d += WV * 64) qs[d] = to_f32(((const T*)a.q)[(size_t)b * a.hidden + head * hd + d]);
   __syncthreads();
   const float slope = a.slopes[head];
@@ -1023,7 +1079,7 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   float m_run = -INFINITY, l_run = 0.f;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (; c < nch; c += WV * nsplit) {
-    if (c != w + WV * sp) load_chunk(c);
+    if (c != w + WV * sp) load_chunk(c, nlast);
     float sc[16];
 #pragma unroll
     for (int it = 0; it < 16; it++) {
@@ -1093,10 +1149,15 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
     if (threadIdx.x < hd) ctx[threadIdx.x] = from_f32<T>(o / L);
     return;
   }
-  // ---- split partial (sc1 write-through), ticket, last arriver merges
   const size_t pair = (size_t)(a.slot + b) * a.n_head + head;
   float* pacc_g = a.part_acc + pair * a.max_chunks * hd;  // [nsplit][hd]
   float* pml_g = a.part_ml + pair * a.max_chunks * 2;     // [nsplit][2]
+  if (a.defer_merge) {  // the consumer merges (attn_merge.h): plain stores, the kernel boundary publishes
+    if (threadIdx.x < hd) pacc_g[sp * hd + threadIdx.x] = o;
+    if (threadIdx.x == 0) { pml_g[sp * 2] = M; pml_g[sp * 2 + 1] = L; }
+    return;
+  }
+  // ---- split partial (sc1 write-through), ticket, last arriver merges
   if (threadIdx.x < hd)
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), attn_rsrc(pacc_g), (uint32_t)(sp * hd + threadIdx.x) * 4, 0, 16);
   if (threadIdx.x == 0) {
@@ -1353,20 +1414,27 @@ size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, 
   return (size_t)B * n_head * mc * (head_dim + 2);
 }
 
+// One 8-wave block per (row, head) when that already fills the chip or the cache is short;
+// otherwise 4-wave blocks split the context so ~256 blocks stream the KV cache (>= one 64-position
+// chunk per wave at full cache).  Static per (B, n_head, cache size), so the consumer of a deferred
+// merge knows it without a device round trip.
+int attention_decode_splits(int B, int n_head, int max_chunks) {
+  const int pairs = B * n_head;
+  if (pairs >= 192 || max_chunks <= 4) return 1;
+  const int nsplit = min((256 + pairs - 1) / pairs, (max_chunks + 3) / 4);
+  return max(1, min(nsplit, 64));
+}
+
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
   if (a.S == 1) {
-    // One 8-wave block per (row, head) when that already fills the chip; otherwise 4-wave blocks
-    // split the context so ~256 blocks stream the KV cache, and the last split of each (row, head)
-    // merges in the same launch (no merge kernel, no extra boundary).
-    const int pairs = a.B * a.n_head;
-    if (pairs >= 192 || a.max_chunks <= 4) {
+    // Split partials merge either in the consumer (defer_merge, attn_merge.h) or, by ticket, in
+    // the last split block of each (row, head) in this launch (no merge kernel either way).
+    const int nsplit = attention_decode_splits(a.B, a.n_head, a.max_chunks);
+    if (nsplit == 1) {
       dim3 g(a.n_head, a.B, 1);
       if (is_bf16) attn_decode_kernel<bf16, 8><<<g, 512, 0, s>>>(a);
       else attn_decode_kernel<float, 8><<<g, 512, 0, s>>>(a);
     } else {
-      int nsplit = (256 + pairs - 1) / pairs;
-      nsplit = min(nsplit, (a.max_chunks + 3) / 4);
-      nsplit = max(1, min(nsplit, 64));
       dim3 g(a.n_head, a.B, nsplit);
       if (is_bf16) attn_decode_kernel<bf16, 4><<<g, 256, 0, s>>>(a);
       else attn_decode_kernel<float, 4><<<g, 256, 0, s>>>(a);

@@ -742,6 +742,9 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     a.B = B; a.S = S; a.slot = slot; a.past = past; a.past_dev = past_dev; a.n_head = nh; a.head_dim = hd;
     a.max_ctx = d.max_ctx; a.hidden = h; a.inv_norm = inv_norm; a.part_acc = s->part_acc; a.part_ml = s->part_ml;
     a.max_chunks = s->max_chunks; a.chunk = s->chunk; a.tickets = s->att_tickets;
+    // a split decode context merges in the dense GEMV's prologue when that kernel can take it
+    const int nsplit = S == 1 ? attention_decode_splits(B, nh, s->max_chunks) : 1;
+    a.defer_merge = s->bf16 && nsplit > 1 && linear_parts_supported(M, h, hd, nsplit);
     {
       ProfScope p(s, st, 3, (double)B * nh * (double)(past + S) * hd * 2 * s->esz);
       launch_attention(s->bf16, a, st);
@@ -749,7 +752,13 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     // a = x + dense(ctx)
     Epi e2{};
     e2.kind = EPI_RESID; e2.bias = w.t[T_DENSE_B]; e2.out_f32 = s->attn; e2.resid = cur; e2.ldo = h;
-    linear(s, st, s->ctx, w.t[T_DENSE_W], M, h, h, e2, 4);
+    if (a.defer_merge) {
+      const AttnParts parts{s->part_acc, s->part_ml, nsplit, nh, hd, s->max_chunks, slot};
+      ProfScope p(s, st, 1, gemv_bytes(s, M, h, h, 4));
+      launch_linear_parts(parts, w.t[T_DENSE_W], M, h, h, e2, st);
+    } else {
+      linear(s, st, s->ctx, w.t[T_DENSE_W], M, h, h, e2, 4);
+    }
     // x2 = LN_post(a); g = gelu(x2 W1 + b1)
     Epi e3{};
     e3.kind = EPI_GELU; e3.bias = w.t[T_FC1_B]; e3.out_act = s->g; e3.ldo = 4 * h;
