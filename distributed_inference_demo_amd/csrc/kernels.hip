@@ -178,6 +178,46 @@ __device__ __forceinline__ void epi_store(const Epi& e, int m, int n, float v) {
   }
 }
 
+// Epilogue operands that do not depend on the GEMV result (bias, residual, past_len): a GEMV whose
+// output lane is known up front loads them at kernel start, so the epilogue is not one more memory
+// round trip after the reduction (decode GEMVs are latency-bound; each round trip is ~1 us).
+struct EpiPre {
+  float bias, resid;
+  int past;
+};
+
+template <typename T>
+__device__ __forceinline__ EpiPre epi_prefetch(const Epi& e, int m, int n, bool valid) {
+  EpiPre p{0.f, 0.f, 0};
+  if (!valid || e.kind == EPI_ARGMAX) return p;
+  p.bias = to_f32(((const T*)e.bias)[n]);
+  if (e.kind == EPI_RESID) p.resid = e.resid[(size_t)m * e.ldo + n];
+  if (e.kind == EPI_QKV) p.past = e.past_dev ? *e.past_dev : e.past;
+  return p;
+}
+
+// epi_store with the operands from epi_prefetch (same arithmetic, same roundings).
+template <typename T, int KIND>
+__device__ __forceinline__ void epi_store_pre(const Epi& e, int m, int n, float v, const EpiPre& p) {
+  if constexpr (KIND == EPI_QKV) {
+    v += p.bias;
+    const int three = 3 * e.head_dim;
+    const int head = n / three, r = n - head * three, which = r / e.head_dim, d = r - which * e.head_dim;
+    if (which == 0) {
+      ((T*)e.q_out)[(size_t)m * e.hidden + head * e.head_dim + d] = from_f32<T>(v);
+    } else {
+      const int b = m / e.seq, t = m - b * e.seq;
+      const size_t idx = (((size_t)(e.slot + b) * e.n_head + head) * e.max_ctx + p.past + t) * e.head_dim + d;
+      T* c = (T*)(which == 1 ? e.k_cache : e.v_cache);
+      c[idx] = from_f32<T>(v);
+    }
+  } else if constexpr (KIND == EPI_RESID) {
+    e.out_f32[(size_t)m * e.ldo + n] = (v + p.bias) + p.resid;
+  } else if constexpr (KIND == EPI_GELU) {
+    ((T*)e.out_act)[(size_t)m * e.ldo + n] = from_f32<T>(gelu_bloom(v + p.bias));
+  }
+}
+
 // Apply the epilogue of compile-time kind K to one element (argmax needs all 64 lanes).
 template <typename T, int K>
 __device__ __forceinline__ void epi_apply(const Epi& ep, int m, int n, float v, bool valid, int ntiles) {
@@ -392,6 +432,12 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_mfma_kernel(const bf16* __res
 // ------------------------------------------------------------------------------------
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
+template <int NT>
+__device__ __forceinline__ bf16x8 wload(const bf16* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
+  else return *reinterpret_cast<const bf16x8*>(p);
+}
+
 __device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float acc) {
   acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[0], a[1]}, (bf16x2){b[0], b[1]}, acc, false);
   acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[2], a[3]}, (bf16x2){b[2], b[3]}, acc, false);
@@ -401,11 +447,13 @@ __device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float ac
 }
 
 // LayerNorm of M <= MM <= 4 rows (K <= 4096) into LDS as bf16, 256 threads, nn.LayerNorm
-// semantics.  Each thread keeps its <= 16 values per row in registers: one global pass, two
-// block reductions (mean, then the exact centred variance), normalise from registers.  Split in
-// two so a kernel can put its own loads (the weight stream) between the row loads and the math.
+// semantics.  Each thread keeps its <= 16 values per row in registers: one global pass, ONE block
+// reduction of the shifted sums (x - c, (x - c)^2 with c = the row's first element, which keeps
+// the one-pass variance free of cancellation when |mean| >> std), normalise from registers.  Split
+// in two so a kernel can put its own loads (the weight stream) between the row loads and the math.
 template <int MM>
-__device__ __forceinline__ void ln_rows_load(const LnArgs& ln, int M, int K, float4 (&xv)[MM][4], uint2 (&gb)[4][2]) {
+__device__ __forceinline__ void ln_rows_load(const LnArgs& ln, int M, int K, float4 (&xv)[MM][4], float (&c)[MM],
+                                             uint2 (&gb)[4][2]) {
 #pragma unroll
   for (int i = 0; i < 4; i++) {  // gamma/beta with the rows: no round trip after the reductions
     const int k = threadIdx.x * 4 + i * 1024;
@@ -415,6 +463,7 @@ __device__ __forceinline__ void ln_rows_load(const LnArgs& ln, int M, int K, flo
 #pragma unroll
   for (int m = 0; m < MM; m++) {
     const float* xr = ln.x + ((size_t)min(m, M - 1) * ln.row_stride + ln.row_offset) * K;
+    c[m] = xr[0];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const int k = threadIdx.x * 4 + i * 1024;
@@ -425,48 +474,41 @@ __device__ __forceinline__ void ln_rows_load(const LnArgs& ln, int M, int K, flo
 
 template <int MM>
 __device__ __forceinline__ void ln_rows_finish(const LnArgs& ln, int M, int K, float4 (&xv)[MM][4],
-                                               const uint2 (&gb)[4][2], bf16* xs, float* scratch) {
+                                               const float (&c)[MM], const uint2 (&gb)[4][2], bf16* xs,
+                                               float* scratch) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float part[MM];
+  float s1[MM], s2[MM];
 #pragma unroll
   for (int m = 0; m < MM; m++) {
-    float acc = 0.f;
+    float a1 = 0.f, a2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; i++) acc += (xv[m][i].x + xv[m][i].y) + (xv[m][i].z + xv[m][i].w);
-    part[m] = wave_sum(acc);
+    for (int i = 0; i < 4; i++) {
+      if (threadIdx.x * 4 + i * 1024 < K) {
+        const float d0 = xv[m][i].x - c[m], d1 = xv[m][i].y - c[m], d2 = xv[m][i].z - c[m], d3 = xv[m][i].w - c[m];
+        a1 += (d0 + d1) + (d2 + d3);
+        a2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+      }
+    }
+    s1[m] = wave_sum(a1);
+    s2[m] = wave_sum(a2);
   }
   if (lane == 0) {
 #pragma unroll
-    for (int m = 0; m < MM; m++) scratch[16 + w * 8 + m] = part[m];
+    for (int m = 0; m < MM; m++) {
+      scratch[w * 8 + m] = s1[m];
+      scratch[32 + w * 8 + m] = s2[m];
+    }
   }
   __syncthreads();
   float mean[MM], rstd[MM];
-#pragma unroll
-  for (int m = 0; m < MM; m++)
-    mean[m] = (scratch[16 + m] + scratch[24 + m] + scratch[32 + m] + scratch[40 + m]) / (float)K;
+  const float invk = 1.0f / (float)K;
 #pragma unroll
   for (int m = 0; m < MM; m++) {
-    float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int k = threadIdx.x * 4 + i * 1024;
-      if (k < K) {
-        const float d0 = xv[m][i].x - mean[m], d1 = xv[m][i].y - mean[m], d2 = xv[m][i].z - mean[m],
-                    d3 = xv[m][i].w - mean[m];
-        acc += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-      }
-    }
-    part[m] = wave_sum(acc);
+    const float t1 = ((scratch[m] + scratch[8 + m]) + (scratch[16 + m] + scratch[24 + m])) * invk;
+    const float t2 = ((scratch[32 + m] + scratch[40 + m]) + (scratch[48 + m] + scratch[56 + m])) * invk;
+    mean[m] = c[m] + t1;
+    rstd[m] = 1.0f / sqrtf(fmaxf(t2 - t1 * t1, 0.f) + ln.eps);
   }
-  __syncthreads();
-  if (lane == 0) {
-#pragma unroll
-    for (int m = 0; m < MM; m++) scratch[16 + w * 8 + m] = part[m];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int m = 0; m < MM; m++)
-    rstd[m] = 1.0f / sqrtf((scratch[16 + m] + scratch[24 + m] + scratch[32 + m] + scratch[40 + m]) / (float)K + ln.eps);
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const int k = threadIdx.x * 4 + i * 1024;
@@ -497,7 +539,9 @@ __device__ __forceinline__ void ln_rows_finish(const LnArgs& ln, int M, int K, f
 enum XMode : int { X_PLAIN = 0, X_LN = 1, X_PARTS = 2 };
 constexpr int kPartsPre = 2;  // 4-column groups per thread whose partial loads go out before the weights
 
-template <int R, int MM, int U, int XM>
+// FL: probe flags for tools/gemv_probe.hip (0 in the product): 1 = temporal (not non-temporal) weight loads,
+// 2 = no activation loads (x = 1), 4 = no epilogue (a store that never fires keeps the math).
+template <int R, int MM, int U, int XM, int FL = 0>
 __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
                                                         LnArgs ln, AttnParts pa, int M, int N, int K, Epi ep) {
   constexpr bool LN = XM == X_LN;
@@ -509,12 +553,16 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
   const bf16* wr[R];
 #pragma unroll
   for (int r = 0; r < R; r++) wr[r] = W + (size_t)min(n0 + r, N - 1) * K;
+  // lane j = r * MM + m stores (row r, token m) in the epilogue; its operands go out first
+  const int er = lane / MM, em = lane % MM;
+  const EpiPre pre = epi_prefetch<bf16>(ep, em, n0 + er, lane < R * MM && em < M && n0 + er < N);
   // LN / PARTS: the activation loads are issued first, then the first U chunks of every weight
   // row, then the prologue math runs on the activations (their loads are the oldest, so waiting
   // for them does not wait for the weights) while the weight stream is in flight
   float4 xv[LN ? MM : 1][4];
+  float xc[LN ? MM : 1];
   uint2 gb[4][2];
-  if constexpr (LN) ln_rows_load<MM>(ln, M, K, xv, gb);
+  if constexpr (LN) ln_rows_load<MM>(ln, M, K, xv, xc, gb);
   const int kq = K >> 2, ngroups = M * kq;  // PARTS: 4-column groups of all rows
   PartsRegs pr[XM == X_PARTS ? kPartsPre : 1];
   auto pld1 = [](const float* p, size_t i) { return p[i]; };
@@ -531,12 +579,12 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
   for (int u = 0; u < U; u++) {
     const int k = min(u * 512 + lane * 8, K - 8);
 #pragma unroll
-    for (int r = 0; r < R; r++) wv[u][r] = *reinterpret_cast<const bf16x8*>(wr[r] + k);
+    for (int r = 0; r < R; r++) wv[u][r] = wload<!(FL & 1)>(wr[r] + k);
   }
   const bf16* xg;
   int xstride;
   if constexpr (LN) {
-    ln_rows_finish<MM>(ln, M, K, xv, gb, xs, scratch);
+    ln_rows_finish<MM>(ln, M, K, xv, xc, gb, xs, scratch);
     xg = xs; xstride = K;
   } else if constexpr (XM == X_PARTS) {
     auto put = [&](int g, const PartsRegs& r) {
@@ -575,7 +623,7 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
       for (int u = 0; u < U; u++) {
         const int k = min(kb + u * 512 + lane * 8, K - 8);
 #pragma unroll
-        for (int r = 0; r < R; r++) wv[u][r] = *reinterpret_cast<const bf16x8*>(wr[r] + k);
+        for (int r = 0; r < R; r++) wv[u][r] = wload<!(FL & 1)>(wr[r] + k);
       }
     }
 #pragma unroll
@@ -585,7 +633,9 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
       const int k = min(kk, K - 8);
 #pragma unroll
       for (int m = 0; m < MM; m++) {
-        bf16x8 xv = *reinterpret_cast<const bf16x8*>(xg + (size_t)min(m, M - 1) * xstride + k);
+        bf16x8 xv;
+        if constexpr (FL & 2) xv = (bf16x8){1, 1, 1, 1, 1, 1, 1, 1};
+        else xv = *reinterpret_cast<const bf16x8*>(xg + (size_t)min(m, M - 1) * xstride + k);
         xv = live ? xv : zero8;
 #pragma unroll
         for (int r = 0; r < R; r++) acc[r][m] = dot8(wv[u][r], xv, acc[r][m]);
@@ -623,8 +673,12 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
         for (int r = 0; r < R; r++)
 #pragma unroll
           for (int m = 0; m < MM; m++) v = (lane == r * MM + m) ? acc[r][m] : v;
-        const int r = lane / MM, m = lane % MM, n = n0 + r;
-        if (m < M && n < N) epi_store<bf16, EK>(ep, m, n, v);
+        const int n = n0 + er;
+        if constexpr (FL & 4) {
+          if (v == 12345.f) ep.keys[0] = 1;
+        } else if (em < M && n < N) {
+          epi_store_pre<bf16, EK>(ep, em, n, v, pre);
+        }
       }
     }
   });
@@ -878,12 +932,12 @@ static int gemv_waves(int N, int K) {
   return waves;
 }
 
-template <int R, int MM, int XM, int U = 2>
+template <int R, int MM, int XM, int U = 2, int FL = 0>
 static void gemv_rows_launch(const bf16* X, const LnArgs& ln, const AttnParts& pa, const bf16* W, int M, int N,
                              int K, const Epi& ep, hipStream_t s) {
   const size_t shm = 256 + (XM != X_PLAIN ? (size_t)M * K * sizeof(bf16) : 0);
   const int blocks = (N + 4 * R - 1) / (4 * R);
-  gemv_rows_kernel<R, MM, U, XM><<<blocks, 256, shm, s>>>(W, X, ln, pa, M, N, K, ep);
+  gemv_rows_kernel<R, MM, U, XM, FL><<<blocks, 256, shm, s>>>(W, X, ln, pa, M, N, K, ep);
 }
 
 template <int XM>
@@ -911,7 +965,9 @@ static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const AttnParts&
     }
     return true;
   }
-  const int R = !LN ? 1 : (N >= 12288 ? 4 : (N >= 6144 ? 2 : 1));
+  // rows per wave (tools/gemv_probe.hip, profiles/r01_gemv_probe.log): 2 on short rows, else 1; LN
+  // variants 2-4 on wide N to amortise the per-block LayerNorm prologue
+  const int R = !LN ? (K <= 2048 ? 2 : 1) : (N >= 12288 ? 4 : (N >= 6144 ? 2 : 1));
   // U = 512-element chunks of a row in flight per iteration: an exact divisor of the row's chunk
   // count, so every row streams in whole rounds with no re-loaded tail (K = 1536 -> 3, 6144 -> 12,
   // 4096 -> 8, 16384 -> 8, 2560 -> 5, 1024 -> 2); fallback 4.
@@ -1064,12 +1120,14 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   // ever holds finite values, so their V rows contribute 0 * finite) and before q is staged.
   int c = w + WV * sp;
   if (c < a.max_chunks) load_chunk(c, a.max_ctx - 1);
+  // q, the slope and past_len are independent of each other: all in flight with the first chunk
+  const float slope = a.slopes[head];
+  const float qreg = threadIdx.x < hd ? to_f32(((const T*)a.q)[(size_t)b * a.hidden + head * hd + threadIdx.x]) : 0.f;
   const int past = a.past_dev ? *a.past_dev : a.past;
   const int nk = past + 1, nlast = nk - 1;
   const int nch = (nk + 63) >> 6;
-  for (int d = threadIdx.x; d < hd; d += WV * 64) qs[d] = to_f32(((const T*)a.q)[(size_t)b * a.hidden + head * hd + d]);
+  if (threadIdx.x < hd) qs[threadIdx.x] = qreg;  // hd <= 128 <= WV * 64
   __syncthreads();
-  const float slope = a.slopes[head];
   float qv[8];
   {
     const float4 q0 = *reinterpret_cast<const float4*>(&qs[doff]);

@@ -36,15 +36,16 @@ void lv(const bf16* W, const bf16* X, const LnArgs& ln, int M, int N, int K, con
 
 struct Var { const char* name; Launch f[3]; };  // waves 4/8/16
 void rows_ln(const bf16* W, const bf16* X, const LnArgs& ln, int M, int N, int K, const Epi& ep, hipStream_t s) {
-  gemv_rows_dispatch<true>(X, ln, W, M, N, K, ep, s);
+  gemv_rows_dispatch<X_LN>(X, ln, AttnParts{}, W, M, N, K, ep, s);
 }
 void rows_pl(const bf16* W, const bf16* X, const LnArgs& ln, int M, int N, int K, const Epi& ep, hipStream_t s) {
-  gemv_rows_dispatch<false>(X, ln, W, M, N, K, ep, s);
+  gemv_rows_dispatch<X_PLAIN>(X, ln, AttnParts{}, W, M, N, K, ep, s);
 }
 template <int R, bool LN, int U>
 void rl(const bf16* W, const bf16* X, const LnArgs& ln, int M, int N, int K, const Epi& ep, hipStream_t s) {
-  if (ep.kind == EPI_ARGMAX) { gemv_rows_launch<4, 1, LN, U>(X, ln, W, M, N, K, ep, s); return; }
-  gemv_rows_launch<R, 1, LN, U>(X, ln, W, M, N, K, ep, s);
+  constexpr int XM = LN ? X_LN : X_PLAIN;
+  if (ep.kind == EPI_ARGMAX) { gemv_rows_launch<4, 1, XM, U>(X, ln, AttnParts{}, W, M, N, K, ep, s); return; }
+  gemv_rows_launch<R, 1, XM, U>(X, ln, AttnParts{}, W, M, N, K, ep, s);
 }
 
 #define VARS(LN, NT, PF, U) {#LN "/nt" #NT "/pf" #PF "/u" #U, {lv<4, 1, LN, NT, PF, U>, lv<8, 1, LN, NT, PF, U>, lv<16, 1, LN, NT, PF, U>}}
