@@ -30,6 +30,12 @@ struct Epi {
   unsigned long long* keys;  // [M][N/16]: max over each 16-column tile
   float* logits;          // optional [M][ldo]
   int col_offset;         // vocabulary index of column 0 (head slices)
+  // split-K workspace of the batched GEMV (gemv_tiles): fp32 partials [ks][M][N] (capacity in
+  // floats) and one arrival ticket per 16-column tile (zero between launches).  Null: no split-K.
+  float* sk_ws;
+  unsigned* sk_tickets;
+  size_t sk_cap;
+  int sk_ntickets;
 };
 
 // dtype tag: 0 = fp32, 1 = bf16

@@ -14,6 +14,12 @@
 #include "kernels.h"
 #include "attn_merge.h"
 
+// Buffer descriptor over a whole allocation for write-through / L2-coherent (aux = 16: sc1)
+// accesses: the split partials other workgroups of the same launch read.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)0xFFFFFFFF, 0x00020000);
+}
+
 #include <cstdlib>
 
 // ------------------------------------------------------------------------------------
@@ -534,6 +540,19 @@ __device__ __forceinline__ void ln_rows_finish(const LnArgs& ln, int M, int K, f
   __syncthreads();
 }
 
+// LayerNorm of M fp32 rows (K <= 4096, K % 4 == 0) -> bf16, one 256-thread block per row, the row
+// held in registers (one global pass, one block reduction): the producer of a batched GEMV's input.
+__global__ __launch_bounds__(256) void ln_rows_kernel(LnArgs ln, int K, bf16* __restrict__ out) {
+  __shared__ float scratch[64];
+  LnArgs lr = ln;
+  lr.x = ln.x + (size_t)blockIdx.x * ln.row_stride * K;
+  float4 xv[1][4];
+  float c[1];
+  uint2 gb[4][2];
+  ln_rows_load<1>(lr, 1, K, xv, c, gb);
+  ln_rows_finish<1>(lr, 1, K, xv, c, gb, out + (size_t)blockIdx.x * K, scratch);
+}
+
 // Activation prologue of gemv_rows_kernel: X read as given, LayerNorm of fp32 rows, or the merge
 // of split-attention partials (attn_merge.h); the last two stage bf16 rows in LDS.
 enum XMode : int { X_PLAIN = 0, X_LN = 1, X_PARTS = 2 };
@@ -682,6 +701,193 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
       }
     }
   });
+}
+
+// ------------------------------------------------------------------------------------
+// gemv_tiles: batched decode GEMV, 4 < M <= 16*MT (bf16 X [M][K], K % 64 == 0).  A block owns T
+// 16-row weight tiles (16T output columns); its WAVES waves split K in 64-wide units.  Per unit a
+// lane (r = lane & 15, g = lane >> 4) streams 32 contiguous bytes of weight row r of every tile
+// (4 lanes x 32 B = one 128-B line per row) and the matching 32 bytes of activation row r of every
+// m-tile, then runs 2 v_mfma_f32_16x16x32_bf16 per (tile, m-tile).  A and B take columns in the same
+// permuted order (k-step j of a unit = columns g*16 + 8j .. +8 of lane g), which leaves every dot
+// product unchanged.  The activation fragments are shared by the T tiles, so activation (L2)
+// traffic is 1/T of a one-tile-per-block design's; the next unit's loads are in flight while this
+// unit's MFMAs run.  Wave partials meet in LDS; the epilogue walks n fastest (coalesced stores,
+// and 16 aligned lanes = one 16-column argmax tile).
+// ------------------------------------------------------------------------------------
+template <int T, int MT, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void gemv_tiles_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
+                                                                int M, int N, int K, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int RS = MT * 16 + 1;  // padded LDS row: [n][m]
+  float* red = reinterpret_cast<float*>(smem);  // [WAVES][T * 16][RS]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * (T * 16);
+  // split-K: block (x, ks) takes units [ks * upb, (ks + 1) * upb), its waves split those
+  const int KS = gridDim.y, ks = blockIdx.y;
+  const int units_all = K >> 6, upb = (units_all + KS - 1) / KS;
+  const int ub0 = min(units_all, ks * upb), units = min(units_all, ub0 + upb) - ub0;
+  const int per = (units + WAVES - 1) / WAVES;
+  const int u0 = ub0 + min(units, w * per), u1 = ub0 + min(units, w * per + per);
+  const bf16* wp[T];
+#pragma unroll
+  for (int t = 0; t < T; t++) wp[t] = W + (size_t)min(n0 + t * 16 + r, N - 1) * K + g * 16;
+  const bf16* xp[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; mt++) xp[mt] = X + (size_t)min(mt * 16 + r, M - 1) * K + g * 16;
+  f32x4 acc[T][MT];
+#pragma unroll
+  for (int t = 0; t < T; t++)
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++) acc[t][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 a[T][2], b[MT][2];
+  auto load = [&](int u, bf16x8 (&aa)[T][2], bf16x8 (&bb)[MT][2]) {
+    const size_t o = (size_t)u * 64;
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+      aa[t][0] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[t] + o));
+      aa[t][1] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[t] + o + 8));
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++) {
+      bb[mt][0] = *reinterpret_cast<const bf16x8*>(xp[mt] + o);
+      bb[mt][1] = *reinterpret_cast<const bf16x8*>(xp[mt] + o + 8);
+    }
+  };
+  if (u0 < u1) load(u0, a, b);
+  for (int u = u0; u < u1; u++) {
+    bf16x8 an[T][2], bn[MT][2];
+    const bool more = u + 1 < u1;
+    if (more) load(u + 1, an, bn);
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+      for (int t = 0; t < T; t++)
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++) acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t][j], b[mt][j], acc[t][mt], 0, 0, 0);
+    if (more) {
+#pragma unroll
+      for (int t = 0; t < T; t++) { a[t][0] = an[t][0]; a[t][1] = an[t][1]; }
+#pragma unroll
+      for (int mt = 0; mt < MT; mt++) { b[mt][0] = bn[mt][0]; b[mt][1] = bn[mt][1]; }
+    }
+  }
+  // D[row = 4g + i (n)][col = r (m)]
+  float* rw = red + (size_t)w * (T * 16) * RS;
+#pragma unroll
+  for (int t = 0; t < T; t++)
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) rw[(t * 16 + 4 * g + i) * RS + mt * 16 + r] = acc[t][mt][i];
+  __syncthreads();
+  const int ntiles = (N + 15) >> 4;
+  constexpr int TOTAL = T * 16 * MT * 16, NTH = WAVES * 64;
+  constexpr int ITER = (TOTAL + NTH - 1) / NTH;
+  float vs[ITER];
+#pragma unroll
+  for (int it = 0; it < ITER; it++) {
+    const int idx = it * NTH + threadIdx.x;
+    const int nl = idx % (T * 16), ml = idx / (T * 16);
+    float v = 0.f;
+    if (idx < TOTAL) {
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ww++) v += red[((size_t)ww * (T * 16) + nl) * RS + ml];
+    }
+    vs[it] = v;
+  }
+  if (KS > 1) {
+    // publish this block's partial tile (write-through), take a ticket; the last of the KS blocks
+    // of this column range sums the KS partials in split order (deterministic) and runs the epilogue
+#pragma unroll
+    for (int it = 0; it < ITER; it++) {
+      const int idx = it * NTH + threadIdx.x;
+      const int nl = idx % (T * 16), ml = idx / (T * 16), n = n0 + nl;
+      if (idx < TOTAL && ml < M && n < N)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vs[it]), attn_rsrc(ep.sk_ws),
+                                              (uint32_t)(((size_t)ks * M + ml) * N + n) * 4, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int sk_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      typedef __attribute__((address_space(1))) unsigned gu32;
+      const unsigned old = __hip_atomic_fetch_add((gu32*)(ep.sk_tickets + blockIdx.x), 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      sk_last = old == (unsigned)(KS - 1);
+      if (sk_last) __hip_atomic_store((gu32*)(ep.sk_tickets + blockIdx.x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!sk_last) return;
+#pragma unroll
+    for (int it = 0; it < ITER; it++) {
+      const int idx = it * NTH + threadIdx.x;
+      const int nl = idx % (T * 16), ml = idx / (T * 16), n = n0 + nl;
+      float v = 0.f;
+      if (idx < TOTAL && ml < M && n < N) {
+        for (int k2 = 0; k2 < KS; k2++)
+          v += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(attn_rsrc(ep.sk_ws),
+                                                                    (uint32_t)(((size_t)k2 * M + ml) * N + n) * 4, 0, 16));
+      }
+      vs[it] = v;
+    }
+  }
+  epi_dispatch(ep.kind, [&](auto kc) {
+    constexpr int EK = decltype(kc)::value;
+#pragma unroll
+    for (int it = 0; it < ITER; it++) {  // uniform trip count: argmax needs every lane
+      const int idx = it * NTH + threadIdx.x;
+      const int nl = idx % (T * 16), ml = idx / (T * 16);
+      const int n = n0 + nl;
+      epi_apply<bf16, EK>(ep, ml, n, vs[it], idx < TOTAL && ml < M && n < N, ntiles);
+    }
+  });
+}
+
+template <int T, int MT, int WAVES>
+static void gemv_tiles_launch(const bf16* X, const bf16* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s) {
+  const size_t shm = sizeof(float) * WAVES * (T * 16) * (MT * 16 + 1);
+  const int blocks = (N + T * 16 - 1) / (T * 16);
+  gemv_tiles_kernel<T, MT, WAVES><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+}
+
+// Shape choice (tools/gemv_probe.hip, PROBE_BATCH): tiles per block 4 / 2 / 1 while the column
+// blocks still cover every CU (>= 256), else 1; narrower N splits K over KS blocks (split-K with a
+// deterministic last-arriver sum) until >= 256 blocks; waves per block 4 / 8 / 16 so every wave
+// keeps >= 4 units (256 columns) of its K range (16 waves only with T = 1: T > 1 spills at 1024
+// threads).
+static bool gemv_tiles_dispatch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s) {
+  if (M <= 4 || M > 32 || (K % 64) != 0) return false;
+  const int T = (N + 63) / 64 >= 256 ? 4 : ((N + 31) / 32 >= 256 ? 2 : 1);
+  const int blocks = (N + T * 16 - 1) / (T * 16), units = K / 64;
+  int KS = 1;
+  if (ep.sk_ws && ep.sk_tickets && blocks <= ep.sk_ntickets)
+    while (blocks * KS < 256 && units / (KS * 2) >= 8 && (size_t)KS * 2 * M * N <= ep.sk_cap) KS *= 2;
+  const int upb = (units + KS - 1) / KS;
+  // 16 waves only for one-tile blocks: wider tiles would spill at 1024 threads per block
+  const int WV = upb >= 64 ? (T == 1 ? 16 : 8) : (upb >= 32 ? 8 : 4);
+  const bool two = M > 16;
+  auto go = [&](auto tc, auto wc) {
+    constexpr int TT = decltype(tc)::value, WW = decltype(wc)::value;
+    if (two) gemv_tiles_launch<TT, 2, WW>(x, w, M, N, K, KS, ep, s);
+    else gemv_tiles_launch<TT, 1, WW>(x, w, M, N, K, KS, ep, s);
+  };
+  auto gw = [&](auto tc) {
+    if (WV == 4) go(tc, EpiKindC<4>{});
+    else if (WV == 8) go(tc, EpiKindC<8>{});
+    else go(tc, EpiKindC<16>{});
+  };
+  if (T == 4) gw(EpiKindC<4>{});
+  else if (T == 2) gw(EpiKindC<2>{});
+  else gw(EpiKindC<1>{});
+  return true;
+}
+
+static bool gemv_tiles_disabled() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("BS_GEMV_TILES_OFF"); v = (e && *e && *e != '0') ? 1 : 0; }
+  return v == 1;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1001,6 +1207,7 @@ template <bool LN>
 static void gemv_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, int M, int N, int K, const Epi& ep,
                           hipStream_t s) {
   if (!gemv_rows_disabled() && gemv_rows_dispatch<LN ? X_LN : X_PLAIN>(x, ln, AttnParts{}, w, M, N, K, ep, s)) return;
+  if (!LN && !gemv_tiles_disabled() && gemv_tiles_dispatch(x, w, M, N, K, ep, s)) return;
   const int waves = gemv_waves(N, K);
   const bool two = M > 16;
   if (waves == 4) { if (two) gemv_launch<4, 2, LN>(x, ln, w, M, N, K, ep, s); else gemv_launch<4, 1, LN>(x, ln, w, M, N, K, ep, s); }
@@ -1014,12 +1221,20 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
                       const void* beta, float eps, void* xn_scratch, const void* W, int M, int N, int K,
                       const Epi& ep, hipStream_t s) {
   if (M <= 0) return;
-  if (is_bf16 && M <= 8 && (K % 8) == 0) {
+  // 4 < M <= 32: a LayerNorm kernel + the tile GEMV beats the per-tile LN-fused GEMV
+  // (tools/gemv_probe.hip batched section)
+  const bool tiles = is_bf16 && M > 4 && M <= 32 && (K % 64) == 0 && !gemv_tiles_disabled();
+  if (is_bf16 && M <= 8 && (K % 8) == 0 && !tiles) {
     LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
     gemv_dispatch<true>(nullptr, ln, (const bf16*)W, M, N, K, ep, s);
     return;
   }
-  launch_layernorm(is_bf16, x, nullptr, row_stride, row_offset, gamma, beta, xn_scratch, 0, M, K, eps, s);
+  if (is_bf16 && K <= 4096 && (K % 4) == 0) {
+    LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
+    ln_rows_kernel<<<M, 256, 0, s>>>(ln, K, (bf16*)xn_scratch);
+  } else {
+    launch_layernorm(is_bf16, x, nullptr, row_stride, row_offset, gamma, beta, xn_scratch, 0, M, K, eps, s);
+  }
   launch_linear(is_bf16, xn_scratch, W, M, N, K, ep, s);
 }
 
@@ -1081,9 +1296,6 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
 // (max, sum, context) partial write-through (sc1) and takes a ticket; the block drawing the last
 // ticket of its (row, head) merges all partials (sc1 loads, issued together) and writes ctx —
 // MI355X_MICROARCH.md "Valid forms" row 1 (counter form, the last adder reads).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)0xFFFFFFFF, 0x00020000);
-}
 
 template <typename T, int WV>
 __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {

@@ -64,6 +64,12 @@ struct ProfClass {
 
 }  // namespace
 
+// Split-K workspace of the batched decode GEMV (kernels.hip gemv_tiles_dispatch): up to 16 splits
+// of 32 rows x 4096 columns, one ticket per 16-column tile.  Used only by enqueue_forward's GEMVs
+// (one stream per stage); head slices on another stream never split K.
+constexpr size_t kSkCap = (size_t)16 * 32 * 4096;
+constexpr int kSkTickets = 4096;
+
 struct bs_stage {
   bs_stage_desc d;
   int bf16 = 1;
@@ -103,6 +109,8 @@ struct bs_stage {
   int* ids = nullptr;                  // [T] staging for host ids
   int* past_dev = nullptr;
   unsigned* att_tickets = nullptr;     // [max_batch][n_head]
+  float* sk_ws = nullptr;              // batched-GEMV split-K partials (kSkCap floats)
+  unsigned* sk_tickets = nullptr;      // [kSkTickets]
   ProfClass prof;
   std::vector<std::pair<void*, size_t>> order;  // canonical weight order (BS_WEIGHTS_HOST layout)
   std::vector<std::pair<GraphKey, hipGraphExec_t>> graphs;  // captured decode steps
@@ -500,6 +508,8 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   wadd(T * 4);
   wadd(256);
   wadd((size_t)desc->max_batch * desc->n_head * 4);  // attention split-merge tickets
+  wadd(kSkCap * 4);                                  // batched-GEMV split-K partials
+  wadd(kSkTickets * 4);                              // and their tickets
   s->wsbytes = woff;
   if (hipMalloc(&s->ws, s->wsbytes) != hipSuccess) return cleanup(fail(BS_ERR_OOM, "workspace allocation failed"));
   int wi = 0;
@@ -518,6 +528,8 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   s->ids = (int*)(s->ws + wo[wi++]);
   s->past_dev = (int*)(s->ws + wo[wi++]);
   s->att_tickets = (unsigned*)(s->ws + wo[wi++]);
+  s->sk_ws = (float*)(s->ws + wo[wi++]);
+  s->sk_tickets = (unsigned*)(s->ws + wo[wi++]);
   HIP_TRY(hipMemsetAsync(s->ws, 0, s->wsbytes, s->own));
   std::vector<float> sl(desc->n_head);
   alibi_slopes(desc->n_head, sl.data());
@@ -657,6 +669,13 @@ static double engine_step_bytes(const bs_stage* s, int B, int past) {
   return b;
 }
 
+// The forward's GEMVs may split K through the stage's workspace (see kSkCap).
+static Epi with_splitk(const bs_stage* s, const Epi& ep) {
+  Epi e = ep;
+  e.sk_ws = s->sk_ws; e.sk_tickets = s->sk_tickets; e.sk_cap = kSkCap; e.sk_ntickets = kSkTickets;
+  return e;
+}
+
 static void linear(bs_stage* s, hipStream_t st, const void* X, const void* W, int M, int N, int K, const Epi& ep,
                    int out_bytes) {
   const bool decode = M <= 32 && s->bf16;
@@ -735,7 +754,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     e.kind = EPI_QKV; e.bias = w.t[T_QKV_B]; e.q_out = s->q; e.k_cache = kbase; e.v_cache = kbase + s->kv_half;
     e.hidden = h; e.head_dim = hd; e.max_ctx = d.max_ctx; e.n_head = nh; e.seq = S; e.slot = slot; e.past = past;
     e.past_dev = past_dev; e.ldo = 3 * h;
-    linear_ln(s, st, cur, 1, 0, w.t[T_LN1_G], w.t[T_LN1_B], w.t[T_QKV_W], M, 3 * h, h, e, 4);
+    linear_ln(s, st, cur, 1, 0, w.t[T_LN1_G], w.t[T_LN1_B], w.t[T_QKV_W], M, 3 * h, h, with_splitk(s, e), 4);
     // attention
     AttnArgs a{};
     a.q = s->q; a.k_cache = kbase; a.v_cache = kbase + s->kv_half; a.ctx_out = s->ctx; a.slopes = s->slopes;
@@ -757,17 +776,17 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
       ProfScope p(s, st, 1, gemv_bytes(s, M, h, h, 4));
       launch_linear_parts(parts, w.t[T_DENSE_W], M, h, h, e2, st);
     } else {
-      linear(s, st, s->ctx, w.t[T_DENSE_W], M, h, h, e2, 4);
+      linear(s, st, s->ctx, w.t[T_DENSE_W], M, h, h, with_splitk(s, e2), 4);
     }
     // x2 = LN_post(a); g = gelu(x2 W1 + b1)
     Epi e3{};
     e3.kind = EPI_GELU; e3.bias = w.t[T_FC1_B]; e3.out_act = s->g; e3.ldo = 4 * h;
-    linear_ln(s, st, s->attn, 1, 0, w.t[T_LN2_G], w.t[T_LN2_B], w.t[T_FC1_W], M, 4 * h, h, e3, (int)s->esz);
+    linear_ln(s, st, s->attn, 1, 0, w.t[T_LN2_G], w.t[T_LN2_B], w.t[T_FC1_W], M, 4 * h, h, with_splitk(s, e3), (int)s->esz);
     // x = a + g W2 + b2
     float* nxt = (!d.is_last && !host_io && l == s->L - 1) ? (float*)out : (cur == s->xa ? s->xb : s->xa);
     Epi e4{};
     e4.kind = EPI_RESID; e4.bias = w.t[T_FC2_B]; e4.out_f32 = nxt; e4.resid = s->attn; e4.ldo = h;
-    linear(s, st, s->g, w.t[T_FC2_W], M, h, 4 * h, e4, 4);
+    linear(s, st, s->g, w.t[T_FC2_W], M, h, 4 * h, with_splitk(s, e4), 4);
     cur = nxt;
   }
 
@@ -782,7 +801,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
       if (rc != BS_OK) return rc;
       e.logits = dev_logits;
     }
-    linear_ln(s, st, cur, S, S - 1, s->lnf_g, s->lnf_b, s->wemb, B, V, h, e, 0);
+    linear_ln(s, st, cur, S, S - 1, s->lnf_g, s->lnf_b, s->wemb, B, V, h, with_splitk(s, e), 0);
     launch_argmax_finalize(s->keys, B, V / 16, nullptr, nullptr, host_io ? s->tok : (int*)out, st);
     if (host_io) {
       HIP_TRY(hipMemcpyAsync(out, s->tok, (size_t)B * 4, hipMemcpyDeviceToHost, st));

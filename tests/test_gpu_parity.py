@@ -119,6 +119,23 @@ def test_batched_decode_with_slot_offset(B):
         tg, to = tg_n, to_n
 
 
+@pytest.mark.parametrize("B", [8, 32])
+def test_batched_decode_real_width_split_k(B):
+    """bloom-1b1 width (h = 1536, 16 heads): the batched tile GEMV with split-K on the N = h GEMVs
+    (dense: 2 splits, fc2: 4 splits), the one-block-per-row LayerNorm feeding it, and the argmax head."""
+    h, nh, L, V = 1536, 16, 1, 2048
+    gs, os_ = pair(h, nh, L, V, 0, L, "bf16", seed=11, max_batch=B, max_ctx=24, max_tokens=B * 4)
+    ids = gen_np.prompt_ids(6, B, 4, V).astype(np.int32)
+    tg = gs.forward_host(ids, B, 4, slot=0, past_len=0)
+    to = os_.forward(ids, B, 4, slot=0, past_len=0)
+    for step in range(3):
+        tg_n, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=0, past_len=4 + step, want_logits=True)
+        to_n, lo = os_.forward(to.reshape(B, 1), B, 1, slot=0, past_len=4 + step, want_logits=True)
+        check_close(lg, lo, "bf16", f"B={B} decode step {step}")
+        assert np.mean(tg_n == to_n) >= 0.9, (step, tg_n, to_n)
+        tg, to = tg_n, to_n
+
+
 def test_prefill_large_gemm_tiles():
     """B*S = 1024 tokens: fc1 goes through the 128x128 MFMA tile, others through 64x64."""
     h, nh, V = 1024, 16, 1024

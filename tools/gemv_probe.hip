@@ -48,6 +48,98 @@ int main() {
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int REPS = 50, ROUNDS = 5;
+  // launch floor: empty kernels of several grid sizes, stream launches vs one captured graph
+  if (getenv("PROBE_LAUNCH")) {
+    hipStream_t st; CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    for (int g : {1, 64, 256, 1024, 4096}) {
+      float best_s = 1e9f, best_g = 1e9f;
+      hipGraph_t gr; hipGraphExec_t ex;
+      CK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+      for (int i = 0; i < REPS; i++) empty_kernel<<<g, 256, 0, st>>>((int*)sink);
+      CK(hipStreamEndCapture(st, &gr)); CK(hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0));
+      for (int r = 0; r < ROUNDS; r++) {
+        float ms;
+        CK(hipEventRecord(e0, st));
+        for (int i = 0; i < REPS; i++) empty_kernel<<<g, 256, 0, st>>>((int*)sink);
+        CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+        best_s = std::min(best_s, ms * 1e3f / REPS);
+        CK(hipGraphLaunch(ex, st));
+        CK(hipEventRecord(e0, st)); CK(hipGraphLaunch(ex, st));
+        CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+        best_g = std::min(best_g, ms * 1e3f / REPS);
+      }
+      printf("empty kernel grid %5d x 256: stream %.2f us/launch, graph %.2f us/launch\n", g, best_s, best_g);
+    }
+    return 0;
+  }
+  // batched decode: the per-tile MFMA GEMV (old) vs the tile GEMV (+ a LayerNorm kernel for LN shapes)
+  if (getenv("PROBE_BATCH")) {
+    struct BS { const char* name; int N, K; bool ln; } bsh[] = {
+      {"1b1 qkv", 4608, 1536, true}, {"1b1 dense", 1536, 1536, false}, {"1b1 fc1", 6144, 1536, true},
+      {"1b1 fc2", 1536, 6144, false}, {"1b1 lm_head", 250880, 1536, true},
+      {"7b1 qkv", 12288, 4096, true}, {"7b1 dense", 4096, 4096, false}, {"7b1 fc1", 16384, 4096, true},
+      {"7b1 fc2", 4096, 16384, false}};
+    bf16* xn; float* xf32; unsigned long long* bkeys;
+    CK(hipMalloc(&xn, 32 * 16384 * 2)); CK(hipMalloc(&xf32, 32 * 16384 * 4)); CK(hipMalloc(&bkeys, 32 * 15680 * 8));
+    float* bout; CK(hipMalloc(&bout, (size_t)32 * 16384 * 4));
+    float* skws; unsigned* sktk;
+    CK(hipMalloc(&skws, (size_t)16 * 32 * 4096 * 4)); CK(hipMalloc(&sktk, 4096 * 4)); CK(hipMemset(sktk, 0, 4096 * 4));
+    fill_f<<<64, 256>>>(xf32, 32 * 16384); fill_rand<<<64, 256>>>(xn, 32 * 16384, 5);
+    CK(hipDeviceSynchronize());
+    for (int M : {8, 32}) {
+      for (auto& sh : bsh) {
+        const int N = sh.N, K = sh.K;
+        Epi ep{};
+        if (N == 250880) { ep.kind = EPI_ARGMAX; ep.keys = bkeys; ep.ldo = N; }
+        else { ep.kind = EPI_RESID; ep.bias = gb; ep.out_f32 = bout; ep.resid = bout; ep.ldo = N; }
+        Epi eps = ep;
+        eps.sk_ws = skws; eps.sk_tickets = sktk; eps.sk_cap = (size_t)16 * 32 * 4096; eps.sk_ntickets = 4096;
+        LnArgs ln{xf32, 1, 0, gb, gb + 16384, 1e-5f};
+        const size_t nk = (size_t)N * K, units = nk > maxW ? 1 : (maxW - nk) / 256 + 1;
+        typedef std::function<void(const bf16*)> F;
+        std::vector<std::pair<std::string, F>> vars;
+        const int waves = gemv_waves(N, K);
+        vars.push_back({"old mfma", [&](const bf16* w) {
+          const bool two = M > 16;
+          if (sh.ln && M <= 8) {
+            if (waves == 4) gemv_launch<4, 1, true>(nullptr, ln, w, M, N, K, ep, 0);
+            else if (waves == 8) gemv_launch<8, 1, true>(nullptr, ln, w, M, N, K, ep, 0);
+            else gemv_launch<16, 1, true>(nullptr, ln, w, M, N, K, ep, 0);
+          } else {
+            if (sh.ln) launch_layernorm(1, xf32, nullptr, 1, 0, gb, gb + 16384, xn, 0, M, K, 1e-5f, 0);
+            if (waves == 4) { if (two) gemv_launch<4, 2, false>(xn, ln, w, M, N, K, ep, 0); else gemv_launch<4, 1, false>(xn, ln, w, M, N, K, ep, 0); }
+            else if (waves == 8) { if (two) gemv_launch<8, 2, false>(xn, ln, w, M, N, K, ep, 0); else gemv_launch<8, 1, false>(xn, ln, w, M, N, K, ep, 0); }
+            else { if (two) gemv_launch<16, 2, false>(xn, ln, w, M, N, K, ep, 0); else gemv_launch<16, 1, false>(xn, ln, w, M, N, K, ep, 0); }
+          }
+        }});
+        vars.push_back({"tiles (+ln_rows)", [&](const bf16* w) {
+          if (sh.ln) ln_rows_kernel<<<M, 256>>>(ln, K, xn);
+          gemv_tiles_dispatch(xn, w, M, N, K, eps, 0);
+        }});
+        if (sh.ln) vars.push_back({"tiles (no LN)", [&](const bf16* w) { gemv_tiles_dispatch(xn, w, M, N, K, eps, 0); }});
+        else vars.push_back({"tiles (no split-K)", [&](const bf16* w) { gemv_tiles_dispatch(xn, w, M, N, K, ep, 0); }});
+        vars.push_back({"stream nt", [&](const bf16* w) { stream_read<1><<<2048, 256>>>((const u32x4*)w, nk * 2 / 16, sink); }});
+        std::vector<std::vector<float>> t(vars.size());
+        for (int r = 0; r < ROUNDS; r++)
+          for (size_t v = 0; v < vars.size(); v++) {
+            for (int i = 0; i < 2; i++) vars[v].second(W);
+            CK(hipEventRecord(e0));
+            for (int i = 0; i < 20; i++) vars[v].second(W + (((size_t)(i + r * 20) * (nk / 256 + 7)) % units) * 256);
+            CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            t[v].push_back(ms * 1e3f / 20);
+          }
+        printf("M=%2d %-12s N=%6d K=%5d  %.1f MB\n", M, sh.name, N, K, nk * 2 / 1e6);
+        for (size_t v = 0; v < vars.size(); v++) {
+          std::sort(t[v].begin(), t[v].end());
+          printf("   %-20s median %8.2f us  %6.0f GB/s\n", vars[v].first.c_str(), t[v][ROUNDS / 2],
+                 nk * 2 / (t[v][ROUNDS / 2] * 1e-6) / 1e9);
+        }
+      }
+    }
+    CK(hipGetLastError());
+    return 0;
+  }
   for (auto& sh : shapes) {
     Epi ep{};
     if (sh.ln) { ep.kind = EPI_GELU; ep.bias = gb; ep.out_act = act; ep.ldo = sh.N; }
