@@ -852,21 +852,34 @@ static void gemv_tiles_launch(const bf16* X, const bf16* W, int M, int N, int K,
   gemv_tiles_kernel<T, MT, WAVES><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
 }
 
-// Shape choice (tools/gemv_probe.hip, PROBE_BATCH): tiles per block 4 / 2 / 1 while the column
-// blocks still cover every CU (>= 256), else 1; narrower N splits K over KS blocks (split-K with a
-// deterministic last-arriver sum) until >= 256 blocks; waves per block 4 / 8 / 16 so every wave
-// keeps >= 4 units (256 columns) of its K range (16 waves only with T = 1: T > 1 spills at 1024
-// threads).
+// Shape choice: the BLOOM shapes take the fastest (tiles, K splits, waves) of the
+// tools/gemv_probe.hip PROBE_SWEEP measurement (profiles/r01_gemv_sweep.log), per m-tile count;
+// other shapes: 2 tiles (4 from N >= 16384), K split until >= 192 blocks while each split keeps
+// >= 8 units, 8 waves when every wave gets >= 2 units.
+struct TileCfg { int N, K, T1, KS1, W1, T2, KS2, W2; };  // (T, KS, waves) for M <= 16 and M <= 32
+static const TileCfg kTileTable[] = {
+  {4608, 1536, 2, 1, 8, 2, 1, 8},    {1536, 1536, 1, 1, 8, 1, 2, 8},   {6144, 1536, 2, 1, 8, 2, 1, 8},
+  {1536, 6144, 2, 4, 8, 2, 4, 8},    {7680, 2560, 2, 1, 8, 2, 1, 8},   {2560, 2560, 1, 1, 8, 1, 1, 8},
+  {10240, 2560, 2, 4, 4, 2, 2, 8},   {2560, 10240, 2, 8, 4, 2, 8, 8},  {12288, 4096, 1, 1, 4, 4, 1, 8},
+  {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 4, 4, 8, 4, 4, 8},
+};
+
 static bool gemv_tiles_dispatch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s) {
   if (M <= 4 || M > 32 || (K % 64) != 0) return false;
-  const int T = (N + 63) / 64 >= 256 ? 4 : ((N + 31) / 32 >= 256 ? 2 : 1);
-  const int blocks = (N + T * 16 - 1) / (T * 16), units = K / 64;
-  int KS = 1;
-  if (ep.sk_ws && ep.sk_tickets && blocks <= ep.sk_ntickets)
-    while (blocks * KS < 256 && units / (KS * 2) >= 8 && (size_t)KS * 2 * M * N <= ep.sk_cap) KS *= 2;
-  const int upb = (units + KS - 1) / KS;
-  // 16 waves only for one-tile blocks: wider tiles would spill at 1024 threads per block
-  const int WV = upb >= 64 ? (T == 1 ? 16 : 8) : (upb >= 32 ? 8 : 4);
+  const int units = K / 64;
+  int T = N >= 16384 ? 4 : 2, KS = 1, WV = 0;
+  for (const TileCfg& c : kTileTable)
+    if (c.N == N && c.K == K) {
+      T = M > 16 ? c.T2 : c.T1; KS = M > 16 ? c.KS2 : c.KS1; WV = M > 16 ? c.W2 : c.W1;
+    }
+  const int blocks = (N + T * 16 - 1) / (T * 16);
+  const bool sk_ok = ep.sk_ws && ep.sk_tickets && blocks <= ep.sk_ntickets;
+  if (WV == 0) {  // not in the table
+    if (sk_ok)
+      while (blocks * KS < 192 && units / (KS * 2) >= 8 && (size_t)KS * 2 * M * N <= ep.sk_cap) KS *= 2;
+    WV = (units + KS - 1) / KS >= 16 ? 8 : 4;
+  }
+  if (KS > 1 && (!sk_ok || (size_t)KS * M * N > ep.sk_cap)) KS = 1;  // no workspace: no split
   const bool two = M > 16;
   auto go = [&](auto tc, auto wc) {
     constexpr int TT = decltype(tc)::value, WW = decltype(wc)::value;
@@ -875,8 +888,7 @@ static bool gemv_tiles_dispatch(const bf16* x, const bf16* w, int M, int N, int 
   };
   auto gw = [&](auto tc) {
     if (WV == 4) go(tc, EpiKindC<4>{});
-    else if (WV == 8) go(tc, EpiKindC<8>{});
-    else go(tc, EpiKindC<16>{});
+    else go(tc, EpiKindC<8>{});
   };
   if (T == 4) gw(EpiKindC<4>{});
   else if (T == 2) gw(EpiKindC<2>{});

@@ -72,6 +72,63 @@ int main() {
     }
     return 0;
   }
+  // sweep of the tile GEMV's (T, KS, waves) per batched shape: best configurations first
+  if (getenv("PROBE_SWEEP")) {
+    struct BS { const char* name; int N, K; } bsh[] = {
+      {"1b1 qkv", 4608, 1536}, {"1b1 dense", 1536, 1536}, {"1b1 fc1", 6144, 1536}, {"1b1 fc2", 1536, 6144},
+      {"3b qkv", 7680, 2560}, {"3b dense", 2560, 2560}, {"3b fc1", 10240, 2560}, {"3b fc2", 2560, 10240},
+      {"7b1 qkv", 12288, 4096}, {"7b1 dense", 4096, 4096}, {"7b1 fc1", 16384, 4096}, {"7b1 fc2", 4096, 16384}};
+    bf16* xn; CK(hipMalloc(&xn, 32 * 16384 * 2)); fill_rand<<<64, 256>>>(xn, 32 * 16384, 5);
+    float* bout; CK(hipMalloc(&bout, (size_t)32 * 16384 * 4));
+    float* skws; unsigned* sktk;
+    const size_t cap = (size_t)16 * 32 * 4096;
+    CK(hipMalloc(&skws, cap * 4)); CK(hipMalloc(&sktk, 4096 * 4)); CK(hipMemset(sktk, 0, 4096 * 4));
+    CK(hipDeviceSynchronize());
+    for (int M : {8, 32}) {
+      for (auto& sh : bsh) {
+        const int N = sh.N, K = sh.K, units = K / 64;
+        Epi ep{};
+        ep.kind = EPI_RESID; ep.bias = gb; ep.out_f32 = bout; ep.resid = bout; ep.ldo = N;
+        ep.sk_ws = skws; ep.sk_tickets = sktk; ep.sk_cap = cap; ep.sk_ntickets = 4096;
+        const size_t nk = (size_t)N * K, rot = (maxW - nk) / 256 + 1;
+        std::vector<std::pair<float, std::string>> res;
+        for (int T : {1, 2, 4})
+          for (int KS : {1, 2, 4, 8})
+            for (int WV : {4, 8, 16}) {
+              if (WV == 16 && T != 1) continue;
+              if ((size_t)KS * M * N > cap || units / KS < WV || (N / (16 * T)) > 4096) continue;
+              auto f = [&](const bf16* w) {
+                const bool two = M > 16;
+#define TL(TT, WW) do { if (two) gemv_tiles_launch<TT, 2, WW>(xn, w, M, N, K, KS, ep, 0); else gemv_tiles_launch<TT, 1, WW>(xn, w, M, N, K, KS, ep, 0); } while (0)
+                if (T == 1) { if (WV == 4) TL(1, 4); else if (WV == 8) TL(1, 8); else TL(1, 16); }
+                else if (T == 2) { if (WV == 4) TL(2, 4); else TL(2, 8); }
+                else { if (WV == 4) TL(4, 4); else TL(4, 8); }
+#undef TL
+              };
+              std::vector<float> t;
+              for (int r = 0; r < 3; r++) {
+                f(W);
+                CK(hipEventRecord(e0));
+                for (int i = 0; i < 20; i++) f(W + (((size_t)(i + r * 20) * (nk / 256 + 7)) % rot) * 256);
+                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+                t.push_back(ms * 1e3f / 20);
+              }
+              std::sort(t.begin(), t.end());
+              char buf[64]; snprintf(buf, sizeof buf, "T=%d KS=%d WV=%d", T, KS, WV);
+              res.push_back({t[1], buf});
+            }
+        std::sort(res.begin(), res.end());
+        const int mine_T = (N + 63) / 64 >= 256 ? 4 : ((N + 31) / 32 >= 256 ? 2 : 1);
+        printf("M=%2d %-10s N=%6d K=%5d %.1f MB:", M, sh.name, N, K, nk * 2 / 1e6);
+        for (size_t i = 0; i < res.size() && i < 4; i++) printf("  %s %.2fus", res[i].second.c_str(), res[i].first);
+        printf("  | worst %s %.2fus\n", res.back().second.c_str(), res.back().first);
+        (void)mine_T;
+      }
+    }
+    CK(hipGetLastError());
+    return 0;
+  }
   // batched decode: the per-tile MFMA GEMV (old) vs the tile GEMV (+ a LayerNorm kernel for LN shapes)
   if (getenv("PROBE_BATCH")) {
     struct BS { const char* name; int N, K; bool ln; } bsh[] = {
