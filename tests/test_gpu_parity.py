@@ -307,3 +307,33 @@ def test_split_kv_decode_attention(dtype):
     for p in (700, 701):
         tok = ids[:, (p * 7) % 700:(p * 7) % 700 + 1]
         check_close(gs.forward_host(tok, B, 1, past_len=p), os_.forward(tok, B, 1, past_len=p), dtype, f"decode past={p}")
+
+
+@pytest.mark.parametrize("B,slot,hd", [(1, 0, 96), (2, 0, 64), (1, 1, 128), (2, 1, 80)])
+def test_small_batch_decode_from_empty_cache(B, slot, hd):
+    """Graph-replayed decode for B <= 2 rows at the real head widths (1b1 96, 560m 64, 7b1 128,
+    3b 80), from an EMPTY cache (past 0: the new position is the whole softmax) through 300
+    positions (1..5 split-attention chunks), with a slot offset — against the oracle, teacher
+    forced, at the listed steps."""
+    import torch
+    nh = 4 if hd != 80 else 8
+    h, L, V = nh * hd, 2, 1024
+    gs, os_ = pair(h, nh, L, V, 0, L, "bf16", seed=31, max_batch=slot + B, max_ctx=320, max_tokens=B * 300)
+    dev = torch.device("cuda", 0)
+    cs = torch.cuda.Stream()
+    with torch.cuda.stream(cs):
+        tok = torch.empty(B, dtype=torch.int32, device=dev)
+        lg = torch.empty((B, V), dtype=torch.float32, device=dev)
+        # from an empty cache: S = 1 at past 0 (the new-position partial is the whole softmax)
+        to = gen_np.prompt_ids(5, B, 1, V).astype(np.int32).reshape(B)
+        past = 0
+        steps = list(range(0, 12)) + [130, 131, 255, 256, 257, 299]
+        for step in range(300):
+            tok.copy_(torch.from_numpy(to))
+            gs.forward(tok, tok, B, 1, slot=slot, past_len=past, logits=lg, stream=cs.cuda_stream)
+            to_next, lo = os_.forward(to.reshape(B, 1), B, 1, past_len=past, slot=slot, want_logits=True)
+            if step in steps:
+                torch.cuda.synchronize()
+                check_close(lg.cpu().numpy(), lo, "bf16", f"fused decode step {step} (ctx {past + 1})")
+            to = to_next
+            past += 1
