@@ -997,17 +997,19 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(const bf16* __restrict__
 }
 
 // ------------------------------------------------------------------------------------
-// gemm_mfma2: prefill GEMM, BM x BN tile (64/128 each), BK = 64, 256 threads as 2x2 waves
-// (wave tile BM/2 x BN/2), register-staged double buffer.  LDS rows are 128 B (64 bf16) with the
-// 16-B chunk index XOR-swizzled by (row & 7), so the 16 rows a ds_read_b128 lane group touches
-// land on different chunk slots.  16 (BN=128) or 8 (BN=64) MFMAs per 32-deep k-step per wave.
+// gemm_mfma2: prefill GEMM, BM x BN tile (32/64/128), BK = 64, 256 threads as 2x2 waves (wave tile
+// BM/2 x BN/2), LDS double buffer fed from a PS-deep ring of register stages: the global loads of
+// tile kt + PS are issued while tile kt computes (one tile of lookahead left the K loop waiting on
+// HBM latency at prefill sizes, where a CU holds only 1-2 blocks).  LDS rows are 128 B (64 bf16)
+// with the 16-B chunk index XOR-swizzled by (row & 7), so the 16 rows a ds_read_b128 lane group
+// touches land on different chunk slots.  MFMA v_mfma_f32_16x16x32_bf16.
 // ------------------------------------------------------------------------------------
-template <int BM, int BN>
+template <int BM, int BN, int PS = 2>
 __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                                          int M, int N, int K, Epi ep) {
   constexpr int BK = 64;
   constexpr int TM = BM / 32, TN = BN / 32;           // 16x16 tiles per wave (wave = BM/2 x BN/2)
-  constexpr int CA = BM * BK / 8 / 256, CB = BN * BK / 8 / 256;  // 16-B chunks per thread: 4, 4|2
+  constexpr int CA = BM * BK / 8 / 256, CB = BN * BK / 8 / 256;  // 16-B chunks per thread: 4, 4|2|1
   __shared__ __attribute__((aligned(16))) bf16 As[2][BM * BK];
   __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * BK];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1029,15 +1031,26 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
     gb[i] = W + (size_t)min(n0 + row, N - 1) * K + ch * 8;
     lb[i] = sw(row, ch);
   }
-  bf16x8 ra[CA], rb[CB];
+  const int nk = K / BK;
+  bf16x8 ra[PS][CA], rb[PS][CB];
+  auto gload = [&](int st, int kt) {  // tile kt -> register stage st (clamped: a re-read past the end is unused)
+    const size_t off = (size_t)min(kt, nk - 1) * BK;
 #pragma unroll
-  for (int i = 0; i < CA; i++) ra[i] = *reinterpret_cast<const bf16x8*>(ga[i]);
+    for (int i = 0; i < CA; i++) ra[st][i] = *reinterpret_cast<const bf16x8*>(ga[i] + off);
 #pragma unroll
-  for (int i = 0; i < CB; i++) rb[i] = *reinterpret_cast<const bf16x8*>(gb[i]);
+    for (int i = 0; i < CB; i++) rb[st][i] = *reinterpret_cast<const bf16x8*>(gb[i] + off);
+  };
+  auto lstore = [&](int st, int buf) {
 #pragma unroll
-  for (int i = 0; i < CA; i++) *reinterpret_cast<bf16x8*>(&As[0][la[i]]) = ra[i];
+    for (int i = 0; i < CA; i++) *reinterpret_cast<bf16x8*>(&As[buf][la[i]]) = ra[st][i];
 #pragma unroll
-  for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(&Bs[0][lb[i]]) = rb[i];
+    for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(&Bs[buf][lb[i]]) = rb[st][i];
+  };
+  // prologue: tiles 0..PS-1 in flight; tile 0 -> LDS; stage 0 refilled with tile PS
+#pragma unroll
+  for (int st = 0; st < PS; st++) gload(st, st);
+  lstore(0, 0);
+  gload(0, PS);
   __syncthreads();
 
   f32x4 acc[TM][TN];
@@ -1046,39 +1059,36 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
 #pragma unroll
     for (int j = 0; j < TN; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / BK;
   int cur = 0;
-  for (int kt = 0; kt < nk; kt++) {
-    const bool more = kt + 1 < nk;
-    if (more) {
+  for (int kt0 = 0; kt0 < nk; kt0 += PS) {
 #pragma unroll
-      for (int i = 0; i < CA; i++) ra[i] = *reinterpret_cast<const bf16x8*>(ga[i] + (size_t)(kt + 1) * BK);
+    for (int s = 0; s < PS; s++) {
+      const int kt = kt0 + s;
+      if (kt < nk) {
 #pragma unroll
-      for (int i = 0; i < CB; i++) rb[i] = *reinterpret_cast<const bf16x8*>(gb[i] + (size_t)(kt + 1) * BK);
+        for (int ks = 0; ks < BK / 32; ks++) {
+          bf16x8 af[TM], bfr[TN];
+#pragma unroll
+          for (int i = 0; i < TM; i++)
+            af[i] = *reinterpret_cast<const bf16x8*>(&As[cur][sw(wm * (BM / 2) + i * 16 + r, ks * 4 + g)]);
+#pragma unroll
+          for (int j = 0; j < TN; j++)
+            bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][sw(wn * (BN / 2) + j * 16 + r, ks * 4 + g)]);
+#pragma unroll
+          for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int j = 0; j < TN; j++)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) {
+          const int nst = (s + 1) % PS;  // stage holding tile kt + 1 (static after the unroll)
+          lstore(nst, cur ^ 1);
+          if (kt + 1 + PS < nk) gload(nst, kt + 1 + PS);
+        }
+        __syncthreads();
+        cur ^= 1;
+      }
     }
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ks++) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; i++)
-        af[i] = *reinterpret_cast<const bf16x8*>(&As[cur][sw(wm * (BM / 2) + i * 16 + r, ks * 4 + g)]);
-#pragma unroll
-      for (int j = 0; j < TN; j++)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][sw(wn * (BN / 2) + j * 16 + r, ks * 4 + g)]);
-#pragma unroll
-      for (int i = 0; i < TM; i++)
-#pragma unroll
-        for (int j = 0; j < TN; j++)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < CA; i++) *reinterpret_cast<bf16x8*>(&As[cur ^ 1][la[i]]) = ra[i];
-#pragma unroll
-      for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(&Bs[cur ^ 1][lb[i]]) = rb[i];
-    }
-    __syncthreads();
-    cur ^= 1;
   }
   const int ntiles = (N + 15) >> 4;
   epi_dispatch(ep.kind, [&](auto kc) {
@@ -1124,6 +1134,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 static bool gemm_v1_forced() {
   static int v = -1;
   if (v < 0) { const char* e = getenv("BS_GEMM_V1"); v = (e && *e && *e != '0') ? 1 : 0; }
+  return v == 1;
+}
+
+static bool gemm_no_narrow() {  // BS_GEMM_NO_NARROW=1: keep 64x64 prefill tiles (A/B switch)
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("BS_GEMM_NO_NARROW"); v = (e && *e && *e != '0') ? 1 : 0; }
   return v == 1;
 }
 
@@ -1277,11 +1293,15 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
     // largest tile that still gives every CU a block (>= 240 blocks), else the smallest
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
     if (blocks(128, 128) >= 240) {
-      gemm_mfma2_kernel<128, 128><<<dim3((N + 127) / 128, (M + 127) / 128), 256, 0, s>>>(x, w, M, N, K, ep);
+      gemm_mfma2_kernel<128, 128, 1><<<dim3((N + 127) / 128, (M + 127) / 128), 256, 0, s>>>(x, w, M, N, K, ep);
     } else if (blocks(128, 64) >= 240) {
-      gemm_mfma2_kernel<128, 64><<<dim3((N + 63) / 64, (M + 127) / 128), 256, 0, s>>>(x, w, M, N, K, ep);
+      gemm_mfma2_kernel<128, 64, 3><<<dim3((N + 63) / 64, (M + 127) / 128), 256, 0, s>>>(x, w, M, N, K, ep);
+    } else if (blocks(64, 64) >= 240 || gemm_no_narrow()) {
+      gemm_mfma2_kernel<64, 64, 4><<<dim3((N + 63) / 64, (M + 63) / 64), 256, 0, s>>>(x, w, M, N, K, ep);
     } else {
-      gemm_mfma2_kernel<64, 64><<<dim3((N + 63) / 64, (M + 63) / 64), 256, 0, s>>>(x, w, M, N, K, ep);
+      // narrow N at prefill sizes (bloom-1b1 dense / fc2 at 512 tokens: 192 64x64 tiles): 64x32
+      // tiles put >= 1 block on every CU, and a second block on many, to hide the K loop's loads
+      gemm_mfma2_kernel<64, 32, 4><<<dim3((N + 31) / 32, (M + 63) / 64), 256, 0, s>>>(x, w, M, N, K, ep);
     }
     return;
   }
@@ -1544,24 +1564,29 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(AttnArgs a) {
 }
 
 // Prefill (S > 1), bf16: MFMA flash attention.  Block = (64-query tile, head, row b), 4 waves x 16
-// queries.  Per 32-key tile: K rows and V^T staged in LDS by the block; S = Q.K^T on
-// v_mfma_f32_16x16x32_bf16 (Q fragments in registers, zero-padded past hd); scale + ALiBi +
-// causal mask + online softmax on the accumulator layout (row = 4*(lane>>4)+i, key = lane&15);
-// P -> fp16 through LDS into the A operand of the P.V MFMAs (v_mfma_f32_16x16x32_f16; V is staged
-// as fp16 — exact for bf16 values in fp16's normal range — so P keeps 10 mantissa bits instead of 7).
-// q is bf16 (the stage stores q in the activation dtype); accumulation and softmax fp32.
+// queries.  Per 64-key tile: K rows and V^T staged in LDS by the block, the NEXT tile's K/V rows
+// already in flight to registers while this one computes (the loop was load-latency bound: one
+// HBM round trip per 32-key tile, 39 us per bloom-1b1 layer at S = 512); S = Q.K^T on
+// v_mfma_f32_16x16x32_bf16 (Q fragments in registers, zero-padded past hd); scale + ALiBi + causal
+// mask + online softmax on the accumulator layout (row = 4*(lane>>4)+i, key = lane&15; row
+// reductions by DPP inside the 16-lane row); P -> fp16 through LDS into the A operand of the P.V
+// MFMAs (v_mfma_f32_16x16x32_f16; V is staged as fp16 — exact for bf16 values in fp16's normal
+// range — so P keeps 10 mantissa bits instead of 7).  q is bf16 (the stage stores q in the
+// activation dtype); accumulation and softmax fp32.  The heaviest query tiles (most keys under
+// the causal mask) are dispatched first.
 template <int HDP>  // head_dim padded to a multiple of 32 (64, 96, 128)
 __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
-  constexpr int KT = 32;                 // keys per tile
+  constexpr int KT = 64;                 // keys per tile
   constexpr int KS = HDP / 32;           // k-steps of S = Q.K^T
   constexpr int NT = HDP / 16;           // 16-dim output tiles
   constexpr int KLD = HDP + 8;           // padded K row (bf16 elements)
   constexpr int VLD = KT + 8;            // padded V^T row
+  constexpr int CPT = (KT * HDP / 8 + 255) / 256;  // 16-B K (and V) chunks per thread per tile
   __shared__ __attribute__((aligned(16))) bf16 Ks[KT * KLD];
   __shared__ __attribute__((aligned(16))) _Float16 Vt[HDP * VLD];
   __shared__ __attribute__((aligned(16))) _Float16 Ps[4][16 * VLD];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
-  const int qt = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
+  const int qt = gridDim.x - 1 - blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int hd = a.head_dim;
   const int past = a.past_dev ? *a.past_dev : a.past;
   const int q0 = qt * 64 + w * 16;          // first query (within this call) of the wave
@@ -1589,31 +1614,48 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   for (int t = 0; t < NT; t++) o[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   // keys visible to the block's last query
   const int kend = past + min(a.S, qt * 64 + 64);
-  const int nchunk = hd / 8;
-  for (int k0 = 0; k0 < kend; k0 += KT) {
-    __syncthreads();  // previous tile's LDS reads are done
-    // stage K rows and V^T: 32 keys x hd, 16-B chunks
-    for (int c = tid; c < KT * nchunk; c += 256) {
+  const int nchunk = hd / 8, nch = KT * nchunk;
+  // the padded dims are never staged: zero them once (keeps the MFMA inputs finite)
+  if (HDP != 0) {
+    for (int c = tid; c < KT * (HDP - hd); c += 256) {
+      const int kr = c / (HDP - hd), d = hd + (c - kr * (HDP - hd));
+      Ks[kr * KLD + d] = (bf16)0.f;
+      Vt[d * VLD + kr] = (_Float16)0.f;
+    }
+  }
+  // V^T row d keeps its 8-key chunks XOR-swizzled by (d >> 3): the transposing element stores of a
+  // wave (lanes = 8-dim slices of a few keys) then spread over the LDS banks instead of two
+  auto vsw = [](int d, int key) { return d * VLD + ((((key >> 3) ^ (d >> 3)) & 7) << 3) + (key & 7); };
+  bf16x8 kreg[CPT], vreg[CPT];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < CPT; i++) {
+      const int c = min(tid + i * 256, nch - 1);
       const int kr = c / nchunk, dc = (c - kr * nchunk) * 8;
       const int key = min(k0 + kr, kend - 1);
-      const bf16x8 kv = *reinterpret_cast<const bf16x8*>(kb + (size_t)key * hd + dc);
-      *reinterpret_cast<bf16x8*>(&Ks[kr * KLD + dc]) = kv;
-      const bf16x8 vv = *reinterpret_cast<const bf16x8*>(vb + (size_t)key * hd + dc);
-#pragma unroll
-      for (int j = 0; j < 8; j++) Vt[(dc + j) * VLD + kr] = (_Float16)(float)vv[j];
+      kreg[i] = *reinterpret_cast<const bf16x8*>(kb + (size_t)key * hd + dc);
+      vreg[i] = *reinterpret_cast<const bf16x8*>(vb + (size_t)key * hd + dc);
     }
-    if (HDP != 0) {  // zero the padded dims once per tile (cheap; keeps the MFMA inputs finite)
-      for (int c = tid; c < KT * (HDP - hd); c += 256) {
-        const int kr = c / (HDP - hd), d = hd + (c - kr * (HDP - hd));
-        Ks[kr * KLD + d] = (bf16)0.f;
-        Vt[d * VLD + kr] = (_Float16)0.f;
+  };
+  gload(0);
+  for (int k0 = 0; k0 < kend; k0 += KT) {
+    __syncthreads();  // previous tile's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < CPT; i++) {
+      const int c = tid + i * 256;
+      if (c < nch) {
+        const int kr = c / nchunk, dc = (c - kr * nchunk) * 8;
+        *reinterpret_cast<bf16x8*>(&Ks[kr * KLD + dc]) = kreg[i];
+#pragma unroll
+        for (int j = 0; j < 8; j++) Vt[vsw(dc + j, kr)] = (_Float16)(float)vreg[i][j];
       }
     }
     __syncthreads();
-    // S tiles: two 16-key tiles
-    f32x4 sacc[2];
+    if (k0 + KT < kend) gload(k0 + KT);  // next tile in flight while this one computes
+    // S tiles: four 16-key tiles
+    f32x4 sacc[4];
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
+    for (int t = 0; t < 4; t++) {
       sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ks++) {
@@ -1622,20 +1664,22 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       }
     }
     // scale, ALiBi, causal mask; lane holds rows 4g+i, key t*16 + r
-    float sv[2][4], rmax[4];
+    float sv[4][4], rmax[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const int qpos = past + q0 + 4 * g + i;
       rmax[i] = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < 2; t++) {
+      for (int t = 0; t < 4; t++) {
         const int kpos = k0 + t * 16 + r;
         const float v = (kpos <= qpos && kpos < kend) ? slope * (float)kpos + a.inv_norm * sacc[t][i] : -INFINITY;
         sv[t][i] = v;
         rmax[i] = fmaxf(rmax[i], v);
       }
-#pragma unroll
-      for (int off = 8; off >= 1; off >>= 1) rmax[i] = fmaxf(rmax[i], __shfl_xor(rmax[i], off, 64));
+      rmax[i] = fmaxf(rmax[i], dpp_f<0xB1>(rmax[i]));  // max over the 16 lanes of the row
+      rmax[i] = fmaxf(rmax[i], dpp_f<0x4E>(rmax[i]));
+      rmax[i] = fmaxf(rmax[i], dpp_f<0x124>(rmax[i]));
+      rmax[i] = fmaxf(rmax[i], dpp_f<0x128>(rmax[i]));
     }
     float scale[4];
 #pragma unroll
@@ -1645,13 +1689,15 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       scale[i] = m_new == -INFINITY ? 1.f : __expf(m_run[i] - m_new);
       float rs = 0.f;
 #pragma unroll
-      for (int t = 0; t < 2; t++) {
+      for (int t = 0; t < 4; t++) {
         const float p = m_new == -INFINITY ? 0.f : __expf(sv[t][i] - m_new);
         sv[t][i] = p;
         rs += p;
       }
-#pragma unroll
-      for (int off = 8; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
+      rs += dpp_f<0xB1>(rs);
+      rs += dpp_f<0x4E>(rs);
+      rs += dpp_f<0x124>(rs);
+      rs += dpp_f<0x128>(rs);
       l_run[i] = l_run[i] * scale[i] + rs;
       m_run[i] = m_new;
     }
@@ -1659,18 +1705,21 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
     for (int t = 0; t < NT; t++)
 #pragma unroll
       for (int i = 0; i < 4; i++) o[t][i] *= scale[i];
-    // P -> LDS (bf16, [16 q][32 keys]) -> A fragment
+    // P -> LDS (fp16, [16 q][64 keys]) -> A fragments
 #pragma unroll
-    for (int t = 0; t < 2; t++)
+    for (int t = 0; t < 4; t++)
 #pragma unroll
       for (int i = 0; i < 4; i++) Ps[w][(4 * g + i) * VLD + t * 16 + r] = (_Float16)sv[t][i];
     __builtin_amdgcn_wave_barrier();
     typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-    const f16x8 pf = *reinterpret_cast<const f16x8*>(&Ps[w][r * VLD + 8 * g]);
+    const f16x8 pf0 = *reinterpret_cast<const f16x8*>(&Ps[w][r * VLD + 8 * g]);
+    const f16x8 pf1 = *reinterpret_cast<const f16x8*>(&Ps[w][r * VLD + 32 + 8 * g]);
 #pragma unroll
     for (int t = 0; t < NT; t++) {
-      const f16x8 vf = *reinterpret_cast<const f16x8*>(&Vt[(t * 16 + r) * VLD + 8 * g]);
-      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, vf, o[t], 0, 0, 0);
+      const f16x8 vf0 = *reinterpret_cast<const f16x8*>(&Vt[vsw(t * 16 + r, 8 * g)]);
+      const f16x8 vf1 = *reinterpret_cast<const f16x8*>(&Vt[vsw(t * 16 + r, 32 + 8 * g)]);
+      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf0, vf0, o[t], 0, 0, 0);
+      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf1, vf1, o[t], 0, 0, 0);
     }
   }
   // write ctx rows (q = q0 + 4g + i, dim = t*16 + r)
