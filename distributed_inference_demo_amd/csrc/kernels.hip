@@ -1046,40 +1046,56 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
 #pragma unroll
     for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(&Bs[buf][lb[i]]) = rb[st][i];
   };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; i++)
+#pragma unroll
+    for (int j = 0; j < TN; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto ktile = [&](int buf) {  // the MFMAs of one BK-deep tile from LDS buffer buf
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ks++) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; i++)
+        af[i] = *reinterpret_cast<const bf16x8*>(&As[buf][sw(wm * (BM / 2) + i * 16 + r, ks * 4 + g)]);
+#pragma unroll
+      for (int j = 0; j < TN; j++)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[buf][sw(wn * (BN / 2) + j * 16 + r, ks * 4 + g)]);
+#pragma unroll
+      for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  int cur = 0;
+  if constexpr (PS == 1) {
+    // one tile of lookahead, loads issued at the top of the step (the 128x128 tile: 2 blocks per
+    // CU hide the rest; a deeper ring costs it occupancy)
+    gload(0, 0);
+    lstore(0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt++) {
+      const bool more = kt + 1 < nk;
+      if (more) gload(0, kt + 1);
+      ktile(cur);
+      if (more) lstore(0, cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
   // prologue: tiles 0..PS-1 in flight; tile 0 -> LDS; stage 0 refilled with tile PS
 #pragma unroll
   for (int st = 0; st < PS; st++) gload(st, st);
   lstore(0, 0);
   gload(0, PS);
   __syncthreads();
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; i++)
-#pragma unroll
-    for (int j = 0; j < TN; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  int cur = 0;
   for (int kt0 = 0; kt0 < nk; kt0 += PS) {
 #pragma unroll
     for (int s = 0; s < PS; s++) {
       const int kt = kt0 + s;
       if (kt < nk) {
-#pragma unroll
-        for (int ks = 0; ks < BK / 32; ks++) {
-          bf16x8 af[TM], bfr[TN];
-#pragma unroll
-          for (int i = 0; i < TM; i++)
-            af[i] = *reinterpret_cast<const bf16x8*>(&As[cur][sw(wm * (BM / 2) + i * 16 + r, ks * 4 + g)]);
-#pragma unroll
-          for (int j = 0; j < TN; j++)
-            bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][sw(wn * (BN / 2) + j * 16 + r, ks * 4 + g)]);
-#pragma unroll
-          for (int i = 0; i < TM; i++)
-#pragma unroll
-            for (int j = 0; j < TN; j++)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
+        ktile(cur);
         if (kt + 1 < nk) {
           const int nst = (s + 1) % PS;  // stage holding tile kt + 1 (static after the unroll)
           lstore(nst, cur ^ 1);
@@ -1089,6 +1105,7 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
         cur ^= 1;
       }
     }
+  }
   }
   const int ntiles = (N + 15) >> 4;
   epi_dispatch(ep.kind, [&](auto kc) {
@@ -1389,10 +1406,10 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; j++) d += qv[j] * raw_get(kr[it], j);
       d = dval ? d : 0.f;
-      d += __shfl_xor(d, 8, 64);
-      d += __shfl_xor(d, 4, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 1, 64);
+      d += dpp_f<0xB1>(d);   // sum over the row's 16 lanes (one DPP row): xor 1, xor 2,
+      d += dpp_f<0x4E>(d);
+      d += dpp_f<0x124>(d);  // rotate 4, rotate 8
+      d += dpp_f<0x128>(d);
       sc[it] = d;
     }
     if (dl == 0) {
