@@ -164,6 +164,9 @@ def bench_single(args):
         if prof_steps:
             st.profile_enable(4 if engine == "persistent" else 1)
             for _ in range(prof_steps):
+                # the eager step's ~100 launches are enqueued behind a spin, so the event pairs time
+                # the GPU's execution, not the host's launch cadence
+                Stage.stream_delay(stream, 3000)
                 st.forward(tok, tok, B, 1, slot=0, past_len=past, stream=stream)
                 past += 1
             g_ms, g_n, g_bytes = st.profile_read()
@@ -204,7 +207,8 @@ def bench_single(args):
                                             "separate rocprofv3 --pmc passes, gfx950 x2 fetch correction; "
                                             f"{note} launches" if traffic else f"traffic unavailable: {note}"),
                            "measured": f"HIP events on the stage stream around each launch, {prof_steps} "
-                                       "decode steps right after the timed region"}
+                                       "eager decode steps right after the timed region, each enqueued "
+                                       "behind a 3 ms stream spin (no host-submission gaps)"}
     res["stage_hbm"] = {"algo_bytes_per_step": step_bytes, "achieved_GBps": step_bytes / (ms_step * 1e-3) / 1e9,
                         "frac_of_peak": step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     res["prefill"] = {"tokens": B * P, "ms": t_prefill * 1e3, "tokens_per_s": B * P / t_prefill,

@@ -613,8 +613,10 @@ extern "C" int bs_profile_enable(bs_stage* s, int32_t cls) {
 
 static hipEvent_t prof_event(bs_stage* s) {
   if (s->prof.used >= s->prof.ev.size()) {
+    // no system-scope fence on the timing markers: a fenced record writes back L2 between the
+    // timed kernels and stretches each ~5 us launch by ~2 us against the kernel trace
     hipEvent_t e;
-    hipEventCreate(&e);
+    hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
     s->prof.ev.push_back(e);
   }
   return s->prof.ev[s->prof.used++];
@@ -632,6 +634,20 @@ extern "C" int bs_profile_read(bs_stage* s, double* total_ms, uint64_t* launches
   if (total_ms) *total_ms = tot;
   if (launches) *launches = s->prof.used / 2;
   if (algo) *algo = s->prof.algo;
+  return BS_OK;
+}
+
+// s_memrealtime ticks at 100 MHz; the spin is bounded by its argument
+__global__ void stream_delay_kernel(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+extern "C" int bs_stream_delay(void* stream, int32_t microseconds) {
+  if (microseconds < 0 || microseconds > 100000) return fail(BS_ERR_INVALID, "delay must be in [0, 100000] us");
+  stream_delay_kernel<<<1, 1, 0, (hipStream_t)stream>>>((long long)microseconds * 100);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BS_ERR_DEVICE, std::string("stream delay: ") + hipGetErrorString(e));
   return BS_OK;
 }
 

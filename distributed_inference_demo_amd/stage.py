@@ -79,7 +79,7 @@ EXPORTS = [
     "bs_stage_weight_count", "bs_abi_version", "bs_profile_enable", "bs_profile_read",
     "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
     "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice", "bs_set_engine", "bs_get_engine",
-    "bs_engine_status", "bs_engine_trace",
+    "bs_engine_status", "bs_engine_trace", "bs_stream_delay",
 ]
 
 ENGINE_AUTO, ENGINE_LAUNCHES, ENGINE_PERSISTENT = 0, 1, 2
@@ -111,6 +111,7 @@ def lib():
         L.bs_profile_enable.argtypes = [vp, i32]
         L.bs_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_double)]
+        L.bs_stream_delay.argtypes = [vp, i32]
         L.bs_codec_serialize.argtypes = [ctypes.POINTER(TensorView), i32, vp, ctypes.c_uint64]
         L.bs_codec_serialize.restype = ctypes.c_int64
         L.bs_codec_deserialize.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(TensorView), i32, ctypes.POINTER(i32)]
@@ -267,6 +268,11 @@ class Stage:
 
     def profile_enable(self, kernel_class):
         _check(lib().bs_profile_enable(self._h, kernel_class))
+
+    @staticmethod
+    def stream_delay(stream, microseconds):
+        """Spin the stream for `microseconds` so the host can enqueue ahead of the GPU."""
+        _check(lib().bs_stream_delay(stream, microseconds))
 
     def profile_read(self):
         ms, n, units = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_double()

@@ -177,6 +177,10 @@ int bs_prompt_ids(uint64_t seed, int32_t n, int32_t vocab, int32_t *out);
  * (or flops for class 2) since the last bs_profile_enable; it synchronizes the stream. */
 int bs_profile_enable(bs_stage *stage, int32_t kernel_class);
 int bs_profile_read(bs_stage *stage, double *total_ms, uint64_t *launches, double *algo_units);
+/* Enqueue a one-thread spin of `microseconds` (<= 100000) on `stream` (hipStream_t; NULL = the
+ * default stream of the current device): lets the host enqueue a whole profiled step behind it,
+ * so event-timed launches are not stretched by host submission gaps. */
+int bs_stream_delay(void *stream, int32_t microseconds);
 
 /* ---- Reference wire codec (utils.cpp:124-368): size_t n; per tensor {int32 dtype,
  * size_t ndim, int64 dims[ndim], raw little-endian data}. size_t is 8 bytes (LP64). ---- */
