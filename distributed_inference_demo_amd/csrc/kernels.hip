@@ -1218,7 +1218,9 @@ static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const AttnParts&
   }
   // rows per wave (tools/gemv_probe.hip, profiles/r01_gemv_probe.log): 2 on short rows, else 1; LN
   // variants 2-4 on wide N to amortise the per-block LayerNorm prologue
-  const int R = !LN ? (K <= 2048 ? 2 : 1) : (N >= 12288 ? 4 : (N >= 6144 ? 2 : 1));
+  // LN-fused: >= 2 rows per wave halves the blocks that each redo the row's LayerNorm
+  // (profiles/r01_ln_rows_sweep.txt: 560m 1566 -> 1621 tok/s, 1b1 1229 -> 1242)
+  const int R = !LN ? (K <= 2048 ? 2 : 1) : (N >= 12288 ? 4 : (N >= 2048 ? 2 : 1));
   // U = 512-element chunks of a row in flight per iteration: an exact divisor of the row's chunk
   // count, so every row streams in whole rounds with no re-loaded tail (K = 1536 -> 3, 6144 -> 12,
   // 4096 -> 8, 16384 -> 8, 2560 -> 5, 1024 -> 2); fallback 4.
