@@ -1348,8 +1348,9 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
 // ticket of its (row, head) merges all partials (sc1 loads, issued together) and writes ctx —
 // MI355X_MICROARCH.md "Valid forms" row 1 (counter form, the last adder reads).
 
-template <typename T, int WV>
+template <typename T, int WV, int CH = 64>  // CH: positions per wave chunk (64 or 32)
 __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
+  constexpr int NI = CH / 4;  // load instructions per chunk (4 rows each)
   __shared__ __attribute__((aligned(16))) float qs[128];
   __shared__ float es[WV][64];
   __shared__ float pm[WV], pl[WV];
@@ -1365,16 +1366,16 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   const bool dval = dl * 8 < hd;
   const int doff = dval ? dl * 8 : 0;  // masked lanes re-read dims 0..7 (harmless)
   typedef typename Raw8<T>::type R8;
-  R8 kr[16], vr[16];
+  R8 kr[NI], vr[NI];
   auto load_chunk = [&](int c, int lim) {
 #pragma unroll
-    for (int it = 0; it < 16; it++) {
-      const int pr = min(c * 64 + it * 4 + grp, lim);
+    for (int it = 0; it < NI; it++) {
+      const int pr = min(c * CH + it * 4 + grp, lim);
       raw_load(kb + (size_t)pr * hd + doff, kr[it]);
     }
 #pragma unroll
-    for (int it = 0; it < 16; it++) {
-      const int pr = min(c * 64 + it * 4 + grp, lim);
+    for (int it = 0; it < NI; it++) {
+      const int pr = min(c * CH + it * 4 + grp, lim);
       raw_load(vb + (size_t)pr * hd + doff, vr[it]);
     }
   };
@@ -1382,13 +1383,13 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   // positions past the context are masked to p = 0 below; the cache is zero-initialised and only
   // ever holds finite values, so their V rows contribute 0 * finite) and before q is staged.
   int c = w + WV * sp;
-  if (c < a.max_chunks) load_chunk(c, a.max_ctx - 1);
+  if (c * CH < a.max_ctx) load_chunk(c, a.max_ctx - 1);
   // q, the slope and past_len are independent of each other: all in flight with the first chunk
   const float slope = a.slopes[head];
   const float qreg = threadIdx.x < hd ? to_f32(((const T*)a.q)[(size_t)b * a.hidden + head * hd + threadIdx.x]) : 0.f;
   const int past = a.past_dev ? *a.past_dev : a.past;
   const int nk = past + 1, nlast = nk - 1;
-  const int nch = (nk + 63) >> 6;
+  const int nch = (nk + CH - 1) / CH;
   if (threadIdx.x < hd) qs[threadIdx.x] = qreg;  // hd <= 128 <= WV * 64
   __syncthreads();
   float qv[8];
@@ -1401,9 +1402,9 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (; c < nch; c += WV * nsplit) {
     if (c != w + WV * sp) load_chunk(c, nlast);
-    float sc[16];
+    float sc[NI];
 #pragma unroll
-    for (int it = 0; it < 16; it++) {
+    for (int it = 0; it < NI; it++) {
       float d = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; j++) d += qv[j] * raw_get(kr[it], j);
@@ -1416,11 +1417,11 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
     }
     if (dl == 0) {
 #pragma unroll
-      for (int it = 0; it < 16; it++) es[w][it * 4 + grp] = sc[it];
+      for (int it = 0; it < NI; it++) es[w][it * 4 + grp] = sc[it];
     }
     __builtin_amdgcn_wave_barrier();
-    const int p = c * 64 + lane;
-    const bool live = p < nk;
+    const int p = c * CH + lane;
+    const bool live = lane < CH && p < nk;
     const float s_me = live ? slope * (float)p + a.inv_norm * es[w][lane] : -INFINITY;
     const float m_new = fmaxf(m_run, wave_max(s_me));
     const float e = live ? __expf(s_me - m_new) : 0.f;
@@ -1433,7 +1434,7 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
     es[w][lane] = e;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int it = 0; it < 16; it++) {
+    for (int it = 0; it < NI; it++) {
       const float ep = es[w][it * 4 + grp];
 #pragma unroll
       for (int j = 0; j < 8; j++) acc[j] += ep * raw_get(vr[it], j);
@@ -1775,6 +1776,12 @@ int attention_decode_splits(int B, int n_head, int max_chunks) {
   return max(1, min(nsplit, 64));
 }
 
+static bool attn_small_chunks() {  // BS_ATTN_CH64=1: keep 4 waves x 64 positions (A/B switch)
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("BS_ATTN_CH64"); v = (e && *e && *e != '0') ? 0 : 1; }
+  return v == 1;
+}
+
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
   if (a.S == 1) {
     // Split partials merge either in the consumer (defer_merge, attn_merge.h) or, by ticket, in
@@ -1784,6 +1791,10 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
       dim3 g(a.n_head, a.B, 1);
       if (is_bf16) attn_decode_kernel<bf16, 8><<<g, 512, 0, s>>>(a);
       else attn_decode_kernel<float, 8><<<g, 512, 0, s>>>(a);
+    } else if (is_bf16 && a.defer_merge && attn_small_chunks()) {
+      // few (row, head) pairs: 8 waves x 32 positions per block, half the serial work per wave
+      dim3 g(a.n_head, a.B, nsplit);
+      attn_decode_kernel<bf16, 8, 32><<<g, 512, 0, s>>>(a);
     } else {
       dim3 g(a.n_head, a.B, nsplit);
       if (is_bf16) attn_decode_kernel<bf16, 4><<<g, 256, 0, s>>>(a);
