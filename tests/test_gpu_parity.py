@@ -337,3 +337,23 @@ def test_small_batch_decode_from_empty_cache(B, slot, hd):
                 check_close(lg.cpu().numpy(), lo, "bf16", f"fused decode step {step} (ctx {past + 1})")
             to = to_next
             past += 1
+
+
+def test_serve_run_on_gpu_matches_oracle_per_sample():
+    """serve.py lifecycle on one GPU (fp32 stage): 5 samples in waves of 2 in flight, each
+    sample's 8 greedy ids equal to the fp32 oracle decoding that sample alone."""
+    import torch
+    from distributed_inference_demo_amd.serve import RunConfig, run_rank, synthetic_prompts
+    model = BloomDims("tinygpu", 256, 2, 4, vocab=1024)  # 2 layers, 4 heads
+    cfg = RunConfig(model=model, num_sample=5, max_length=8, core_pool_size=2, prompt_len=9, dtype="fp32", seed=11)
+    res = run_rank(cfg, 0, 1, torch.device("cuda", 0))
+    want = []
+    for p in synthetic_prompts(cfg, model.vocab):
+        o = OracleStage(256, 4, 2, 1024, 0, 2, bf16=False, max_batch=1, max_ctx=32, seed=11)
+        tok = o.forward(np.array(p, np.int32).reshape(1, -1), 1, len(p))
+        ids = [int(tok[0])]
+        for i in range(cfg.max_length - 1):
+            tok = o.forward(tok.reshape(1, 1), 1, 1, past_len=len(p) + i)
+            ids.append(int(tok[0]))
+        want.append(ids)
+    assert res["samples"] == want

@@ -1,0 +1,73 @@
+"""The server/client run (serve.py) on CPU: num_sample samples in waves of
+core_pool_size micro-batches through 1 or 2 gloo ranks, each sample's max_length greedy ids equal
+to the single-stage oracle decoding that sample alone.  Stage math = the CPU checker (as in
+test_pipeline_gloo.py)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from distributed_inference_demo_amd.serve import RunConfig, run_rank, synthetic_prompts
+from oracle.oracle import OracleStage
+from test_pipeline_gloo import MODEL, SEED, OracleExecutor, _free_port
+
+CFG = RunConfig(model=MODEL, num_sample=5, max_length=6, core_pool_size=2, prompt_len=7, dtype="fp32")
+
+
+def _reference(prompts, max_length):
+    out = []
+    for p in prompts:
+        st = OracleStage(MODEL.hidden, MODEL.n_head, MODEL.n_layer, MODEL.vocab, 0, MODEL.n_layer, max_batch=1,
+                         max_ctx=len(p) + max_length + 1, seed=SEED)
+        tok = st.forward(np.array(p, np.int32).reshape(1, -1), 1, len(p))
+        ids = [int(tok[0])]
+        for i in range(max_length - 1):
+            tok = st.forward(tok.reshape(1, 1), 1, 1, past_len=len(p) + i)
+            ids.append(int(tok[0]))
+        out.append(ids)
+    return out
+
+
+def _worker(rank, world, port, q, head_split):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = RunConfig(**{**CFG.__dict__, "head_split": head_split})
+        res = run_rank(cfg, rank, world, torch.device("cpu"), executor_factory=OracleExecutor)
+        if rank == 0:
+            q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("head_split", [False, True])
+def test_serve_two_ranks_matches_per_sample_oracle(head_split):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, head_split)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res["num_sample"] == 5 and res["stages"] == 2 and len(res["samples"]) == 5
+    assert res["samples"] == _reference(synthetic_prompts(CFG, MODEL.vocab), CFG.max_length)
+
+
+def test_serve_single_rank_given_prompts():
+    rng = np.random.default_rng(5)
+    prompts = rng.integers(0, MODEL.vocab, size=(3, 4)).tolist()
+    cfg = RunConfig(**{**CFG.__dict__, "num_sample": 3, "core_pool_size": 2, "max_length": 4})
+    res = run_rank(cfg, 0, 1, torch.device("cpu"), prompts=prompts, executor_factory=OracleExecutor)
+    assert res["prompt_len"] == 4 and res["samples"] == _reference(prompts, 4)
+
+
+def test_serve_rejects_ragged_prompts():
+    with pytest.raises(ValueError):
+        run_rank(RunConfig(**{**CFG.__dict__, "num_sample": 2}), 0, 1, torch.device("cpu"), prompts=[[1, 2], [3]],
+                 executor_factory=OracleExecutor)
