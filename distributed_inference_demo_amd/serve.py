@@ -9,9 +9,10 @@ num_device, graph, ...}, places contiguous layer ranges with `round_robin_module
 
 Here: one process per GPU (torchrun), rank r = device r of the graph, layers from the same
 placement (`placement.stage_ranges`).  Lifecycle:
-  init   — RunConfig -> this rank's stage + Pipeline (`pipeline.build_rank`), `core_pool_size`
-           micro-batches of one sample each (each owns its KV slot);
-  run    — samples in waves of `core_pool_size`: one prompt prefill round, then max_length - 1
+  init   — RunConfig -> this rank's stage + Pipeline (`pipeline.build_rank`); the `core_pool_size`
+           samples in flight = min(pool, stages) micro-batches x the rest as rows (each sample
+           owns a KV slot), so every stage computes while the hops overlap;
+  run    — samples in waves of the pool: one prompt prefill round, then max_length - 1
            decode rounds, all micro-batches in flight through the stages (a short last wave is
            padded with copies of its last sample, whose outputs are dropped);
   finish — rank 0 returns every sample's `max_length` greedy token ids and the run's tokens/s.
@@ -80,12 +81,17 @@ def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory
             t = t.to(device)
         dist.broadcast(t, src=0)
         plen = int(t.item())
-    n_mb = cfg.core_pool_size
+    # samples in flight = n_mb micro-batches x mb rows: one micro-batch per stage keeps every stage
+    # busy; the rest of the pool rides as rows of a micro-batch (one GPU: one batched decode)
+    n_mb = min(cfg.core_pool_size, world)
+    mb = -(-cfg.core_pool_size // n_mb)
+    pool = n_mb * mb
     # ---- init (Ready)
-    pipe, (lb, le) = build_rank(model, rank, world, device, dtype=cfg.dtype, mb_rows=1, n_mb=n_mb,
+    pipe, (lb, le) = build_rank(model, rank, world, device, dtype=cfg.dtype, mb_rows=mb, n_mb=n_mb,
                                 max_ctx=plen + cfg.max_length + 1, max_seq=plen, seed=cfg.seed,
                                 head_split=cfg.head_split, executor_factory=executor_factory)
-    say(STATES[0], {"rank_layers": [lb, le], "stages": world, "core_pool_size": n_mb})
+    say(STATES[0], {"rank_layers": [lb, le], "stages": world, "core_pool_size": cfg.core_pool_size,
+                    "micro_batches": n_mb, "rows_per_micro_batch": mb})
     cuda = device.type == "cuda"
     if cuda:
         torch.cuda.set_stream(torch.cuda.Stream(device))  # decode steps are captured as hipGraphs
@@ -95,11 +101,11 @@ def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory
     say(STATES[1], {"num_sample": cfg.num_sample, "max_length": cfg.max_length})
     out = []
     t0 = time.perf_counter()
-    for w0 in range(0, cfg.num_sample, n_mb):
+    for w0 in range(0, cfg.num_sample, pool):
         prompt = None
         if rank == 0:
-            wave = prompts[w0:w0 + n_mb]
-            wave = wave + [wave[-1]] * (n_mb - len(wave))  # pad a short last wave
+            wave = prompts[w0:w0 + pool]
+            wave = wave + [wave[-1]] * (pool - len(wave))  # pad a short last wave
             prompt = torch.tensor(wave, dtype=torch.int32, device=device)
         pipe.past = [0] * n_mb  # each micro-batch's slot starts a new sample
         rec = [[] for _ in range(n_mb)] if pipe.is_first else None
@@ -109,7 +115,7 @@ def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory
         pipe.finish(record=rec)
         if rank == 0:
             ids = torch.cat([torch.stack(r, 1) for r in rec], 0).cpu()
-            out.extend(ids[: min(n_mb, cfg.num_sample - w0)].tolist())
+            out.extend(ids[: min(pool, cfg.num_sample - w0)].tolist())
     if cuda:
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -119,7 +125,7 @@ def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory
     if rank != 0:
         return None
     res = {"samples": out, "num_sample": cfg.num_sample, "max_length": cfg.max_length,
-           "core_pool_size": n_mb, "stages": world, "prompt_len": plen, "seconds": dt,
+           "core_pool_size": cfg.core_pool_size, "stages": world, "prompt_len": plen, "seconds": dt,
            "tokens_per_s": cfg.num_sample * cfg.max_length / dt}
     say(STATES[2], {k: v for k, v in res.items() if k != "samples"})
     say(STATES[3], {})
