@@ -1646,7 +1646,11 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   // V^T row d keeps its 8-key chunks XOR-swizzled by (d >> 3): the transposing element stores of a
   // wave (lanes = 8-dim slices of a few keys) then spread over the LDS banks instead of two
   auto vsw = [](int d, int key) { return d * VLD + ((((key >> 3) ^ (d >> 3)) & 7) << 3) + (key & 7); };
-  bf16x8 kreg[CPT], vreg[CPT];
+  // V is staged by (4 keys x 8 dims) items: one 8-B LDS store per dim writes 4 keys of V^T
+  // (a thread per item; KT/4 * hd/8 <= 256 items)
+  const int nvi = (KT / 4) * nchunk;
+  const int vq = min(tid, nvi - 1) / nchunk, vdc = (min(tid, nvi - 1) % nchunk) * 8;
+  bf16x8 kreg[CPT], vreg[4];
   auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < CPT; i++) {
@@ -1654,7 +1658,11 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       const int kr = c / nchunk, dc = (c - kr * nchunk) * 8;
       const int key = min(k0 + kr, kend - 1);
       kreg[i] = *reinterpret_cast<const bf16x8*>(kb + (size_t)key * hd + dc);
-      vreg[i] = *reinterpret_cast<const bf16x8*>(vb + (size_t)key * hd + dc);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int key = min(k0 + vq * 4 + i, kend - 1);
+      vreg[i] = *reinterpret_cast<const bf16x8*>(vb + (size_t)key * hd + vdc);
     }
   };
   gload(0);
@@ -1666,8 +1674,15 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       if (c < nch) {
         const int kr = c / nchunk, dc = (c - kr * nchunk) * 8;
         *reinterpret_cast<bf16x8*>(&Ks[kr * KLD + dc]) = kreg[i];
+      }
+    }
+    if (tid < nvi) {
+      typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int j = 0; j < 8; j++) Vt[vsw(dc + j, kr)] = (_Float16)(float)vreg[i][j];
+      for (int j = 0; j < 8; j++) {
+        const f16x4 v4 = {(_Float16)(float)vreg[0][j], (_Float16)(float)vreg[1][j], (_Float16)(float)vreg[2][j],
+                          (_Float16)(float)vreg[3][j]};
+        *reinterpret_cast<f16x4*>(&Vt[vsw(vdc + j, vq * 4)]) = v4;
       }
     }
     __syncthreads();
