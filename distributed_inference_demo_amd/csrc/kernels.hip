@@ -1309,13 +1309,25 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
     return;
   }
   if ((K % 64) == 0 && !gemm_v1_forced()) {
-    // largest tile that still gives every CU a block (>= 240 blocks), else the smallest
+    // 128x128 when it still gives every CU a block (>= 240 blocks), else 64x64, else 64x32
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-    if (blocks(128, 128) >= 240) {
+    static const int forced = [] {  // BS_GEMM_TILE=1..4: force 128x128 / 128x64 / 64x64 / 64x32 (sweeps)
+      const char* e = getenv("BS_GEMM_TILE");
+      return e && *e ? atoi(e) : 0;
+    }();
+    if (forced == 1) {
       gemm_mfma2_kernel<128, 128, 1><<<dim3((N + 127) / 128, (M + 127) / 128), 256, 0, s>>>(x, w, M, N, K, ep);
-    } else if (blocks(128, 64) >= 240) {
+    } else if (forced == 2) {
       gemm_mfma2_kernel<128, 64, 3><<<dim3((N + 63) / 64, (M + 127) / 128), 256, 0, s>>>(x, w, M, N, K, ep);
+    } else if (forced == 3) {
+      gemm_mfma2_kernel<64, 64, 4><<<dim3((N + 63) / 64, (M + 63) / 64), 256, 0, s>>>(x, w, M, N, K, ep);
+    } else if (forced == 4) {
+      gemm_mfma2_kernel<64, 32, 4><<<dim3((N + 31) / 32, (M + 63) / 64), 256, 0, s>>>(x, w, M, N, K, ep);
+    } else if (blocks(128, 128) >= 240) {
+      gemm_mfma2_kernel<128, 128, 1><<<dim3((N + 127) / 128, (M + 127) / 128), 256, 0, s>>>(x, w, M, N, K, ep);
     } else if (blocks(64, 64) >= 240 || gemm_no_narrow()) {
+      // below 240 128x128 tiles the K loop is latency-bound: 64x64 tiles with a 4-deep ring beat
+      // 128x64 (profiles/r01_gemm_tile_sweep.txt: bloom-1b1 S=512 prefill 4.56 -> 4.42 ms)
       gemm_mfma2_kernel<64, 64, 4><<<dim3((N + 63) / 64, (M + 63) / 64), 256, 0, s>>>(x, w, M, N, K, ep);
     } else {
       // narrow N at prefill sizes (bloom-1b1 dense / fc2 at 512 tokens: 192 64x64 tiles): 64x32
