@@ -1220,7 +1220,8 @@ static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const AttnParts&
   // variants 2-4 on wide N to amortise the per-block LayerNorm prologue
   // LN-fused: >= 2 rows per wave halves the blocks that each redo the row's LayerNorm
   // (profiles/r01_ln_rows_sweep.txt: 560m 1566 -> 1621 tok/s, 1b1 1229 -> 1242)
-  const int R = !LN ? (K <= 2048 ? 2 : 1) : (N >= 12288 ? 4 : (N >= 2048 ? 2 : 1));
+  static const int plain_r = [] { const char* e = getenv("BS_PLAIN_R"); return e && *e ? atoi(e) : 0; }();  // sweeps
+  const int R = !LN ? (plain_r ? plain_r : (K <= 2048 ? 2 : 1)) : (N >= 12288 ? 4 : (N >= 2048 ? 2 : 1));
   // U = 512-element chunks of a row in flight per iteration: an exact divisor of the row's chunk
   // count, so every row streams in whole rounds with no re-loaded tail (K = 1536 -> 3, 6144 -> 12,
   // 4096 -> 8, 16384 -> 8, 2560 -> 5, 1024 -> 2); fallback 4.
@@ -1797,6 +1798,8 @@ size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, 
 // chunk per wave at full cache).  Static per (B, n_head, cache size), so the consumer of a deferred
 // merge knows it without a device round trip.
 int attention_decode_splits(int B, int n_head, int max_chunks) {
+  static const int forced = [] { const char* e = getenv("BS_ATTN_SPLITS"); return e && *e ? atoi(e) : 0; }();  // sweeps
+  if (forced > 0) return min(forced, max(1, max_chunks));
   const int pairs = B * n_head;
   if (pairs >= 192 || max_chunks <= 4) return 1;
   const int nsplit = min((256 + pairs - 1) / pairs, (max_chunks + 3) / 4);
