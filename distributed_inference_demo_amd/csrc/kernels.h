@@ -36,6 +36,9 @@ struct Epi {
   unsigned* sk_tickets;
   size_t sk_cap;
   int sk_ntickets;
+  // int8 weights: y[m][n] *= col_scale[n] before the epilogue (the weight operand held Q, not
+  // Q * scale).  Null otherwise.  Not applied by EPI_ARGMAX.
+  const float* col_scale;
 };
 
 // dtype tag: 0 = fp32, 1 = bf16
@@ -99,3 +102,15 @@ void launch_linear_parts(const AttnParts& p, const void* W, int M, int N, int K,
 void launch_argmax_finalize(const unsigned long long* keys, int M, int ntiles, const unsigned long long* keys_in,
                             unsigned long long* keys_out, int* tokens, hipStream_t s);
 void launch_set_past(int* past_dev, int value, hipStream_t s);
+
+// ---- Weight-only int8 (bf16 stages with BS_FLAG_INT8_WEIGHTS; kernels.hip "Weight-only int8") ----
+// Q[n][k] = rne(W[n][k] / scale[n]), scale[n] = max_k |W[n][k]| / 127 (1 for a zero row); W bf16 [N][K].
+void launch_quantize_rows(const void* W_bf16, int8_t* Q, float* scale, int N, int K, hipStream_t s);
+// out bf16 [N][K] = Q * scale (row-wise).
+void launch_dequant_rows(const int8_t* Q, const float* scale, void* out_bf16, int N, int K, hipStream_t s);
+// Does launch_linear_q8 run M rows of a K-wide GEMV straight from the int8 weights?
+bool linear_q8_gemv(int M, int K);
+// X bf16 [M][K] x (Q * scale)^T with epilogue (not EPI_ARGMAX).  M <= 8: int8 GEMV; otherwise Q is
+// dequantized into w_scratch (bf16, N*K) and the bf16 GEMM runs on it.
+void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* w_scratch, int M, int N, int K,
+                      const Epi& ep, hipStream_t s);

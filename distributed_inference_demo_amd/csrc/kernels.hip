@@ -20,6 +20,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)0xFFFFFFFF, 0x00020000);
 }
 
+#include <algorithm>
 #include <cstdlib>
 
 // ------------------------------------------------------------------------------------
@@ -163,6 +164,7 @@ __device__ __forceinline__ void argmax_tile16(const Epi& e, int m, int n, float 
 
 template <typename T, int KIND>
 __device__ __forceinline__ void epi_store(const Epi& e, int m, int n, float v) {
+  if (e.col_scale) v *= e.col_scale[n];
   if constexpr (KIND == EPI_QKV) {
     v += to_f32(((const T*)e.bias)[n]);
     const int three = 3 * e.head_dim;
@@ -205,6 +207,7 @@ __device__ __forceinline__ EpiPre epi_prefetch(const Epi& e, int m, int n, bool 
 // epi_store with the operands from epi_prefetch (same arithmetic, same roundings).
 template <typename T, int KIND>
 __device__ __forceinline__ void epi_store_pre(const Epi& e, int m, int n, float v, const EpiPre& p) {
+  if (e.col_scale) v *= e.col_scale[n];
   if constexpr (KIND == EPI_QKV) {
     v += p.bias;
     const int three = 3 * e.head_dim;
@@ -1887,3 +1890,163 @@ void launch_argmax_finalize(const unsigned long long* keys, int M, int ntiles, c
 
 __global__ void set_past_kernel(int* p, int v) { *p = v; }
 void launch_set_past(int* past_dev, int value, hipStream_t s) { set_past_kernel<<<1, 1, 0, s>>>(past_dev, value); }
+
+// ------------------------------------------------------------------------------------
+// Weight-only int8 (BS_FLAG_INT8_WEIGHTS): the four block matrices of a bf16 stage held as int8
+// [N][K] + one fp32 scale per output row -- the MI355X counterpart of the reference's bloom*-int8
+// modules (server.py:796-799, data/Data.kt:19-30).  Rule (oracle/bloom_oracle.c or_quantize_int8
+// restates it): scale[n] = max_k |W[n][k]| / 127 (1 for an all-zero row), Q[n][k] = rne(W[n][k] /
+// scale[n]) clamped to [-127, 127], W = the bf16 weight the stage would otherwise hold.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void quantize_rows_kernel(const bf16* __restrict__ W, int8_t* __restrict__ Q,
+                                                            float* __restrict__ scale, int K) {
+  const size_t row = blockIdx.x;
+  const bf16* w = W + row * K;
+  float amax = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) amax = fmaxf(amax, fabsf((float)w[k]));
+  amax = wave_max(amax);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float sc = amax > 0.f ? amax / 127.f : 1.f;  // IEEE division (no fast-math in this build)
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const float v = fminf(fmaxf(rintf((float)w[k] / sc), -127.f), 127.f);
+    Q[row * K + k] = (int8_t)(int)v;
+  }
+  if (threadIdx.x == 0) scale[row] = sc;
+}
+
+// out[n][k] = bf16(Q[n][k] * scale[n]) (scale null: Q itself, exact in bf16): operand of the bf16
+// GEMM for prefill / wide batches, whose epilogue then applies the row scale (Epi::col_scale).
+__global__ __launch_bounds__(256) void dequant_rows_kernel(const int8_t* __restrict__ Q, const float* __restrict__ scale,
+                                                           bf16* __restrict__ out, size_t n8, int K) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    const size_t e = i * 8;
+    const float sc = scale ? scale[e / K] : 1.f;
+    const int2 q = *reinterpret_cast<const int2*>(Q + e);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int w = j < 4 ? q.x : q.y;
+      const float v = (float)((w << (24 - 8 * (j & 3))) >> 24) * sc;  // sc = 1: exact Q
+      o[j] = __builtin_bit_cast(unsigned short, (bf16)v);
+    }
+    *reinterpret_cast<u16x8*>(out + e) = o;
+  }
+}
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Decode GEMV on int8 weights, M <= MM <= 8 rows.  A wave owns R weight rows; per step a lane
+// streams 16 int8 weights (16 B, non-temporal) of each of its rows -- half the bytes of the bf16
+// rows GEMV -- and reads the 16 matching bf16 activations of every row m (L2-resident).  fp32
+// FMAs, DPP wave reduction, the row scale applied once to the reduced sum, then the usual epilogue.
+template <int R, int MM, int KIND>
+__device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const float* __restrict__ scale,
+                                             const bf16* __restrict__ X, int M, int N, int K, const Epi& ep) {
+  const int lane = threadIdx.x & 63;
+  const int n0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (n0 >= N) return;
+  float acc[R][MM];
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int m = 0; m < MM; m++) acc[r][m] = 0.f;
+  const int8_t* wr[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) wr[r] = Q + (size_t)min(n0 + r, N - 1) * K;
+  int c = lane * 16;
+  i32x4 wv[R];
+  if (c < K) {
+#pragma unroll
+    for (int r = 0; r < R; r++) wv[r] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c));
+  }
+  for (; c < K; c += 1024) {
+    i32x4 cur[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) cur[r] = wv[r];
+    if (c + 1024 < K) {  // next step's weights in flight during this step's FMAs
+#pragma unroll
+      for (int r = 0; r < R; r++) wv[r] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c + 1024));
+    }
+    float wf[R][16];
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+      for (int j = 0; j < 16; j++) wf[r][j] = (float)((cur[r][j >> 2] << (24 - 8 * (j & 3))) >> 24);
+#pragma unroll
+    for (int m = 0; m < MM; m++) {
+      if (m < M) {
+        u16x8 a0, a1;
+        raw_load(X + (size_t)m * K + c, a0);
+        raw_load(X + (size_t)m * K + c + 8, a1);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+#pragma unroll
+          for (int j = 0; j < 8; j++) acc[r][m] = fmaf(raw_get(a0, j), wf[r][j], acc[r][m]);
+#pragma unroll
+          for (int j = 0; j < 8; j++) acc[r][m] = fmaf(raw_get(a1, j), wf[r][8 + j], acc[r][m]);
+        }
+      }
+    }
+  }
+  float mine = 0.f;
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int m = 0; m < MM; m++) {
+      if (m < M) {
+        const float t = wave_sum(acc[r][m]);
+        if (lane == r * MM + m) mine = t;
+      }
+    }
+  const int r = lane / MM, m = lane - r * MM;
+  if (lane < R * MM && m < M && n0 + r < N) epi_store<bf16, KIND>(ep, m, n0 + r, mine);  // ep.col_scale = scale
+}
+
+template <int R, int MM>
+__global__ __launch_bounds__(256) void gemv_q8_kernel(const int8_t* __restrict__ Q, const float* __restrict__ scale,
+                                                      const bf16* __restrict__ X, int M, int N, int K, Epi ep) {
+  epi_dispatch(ep.kind, [&](auto kc) {
+    if constexpr (decltype(kc)::value != EPI_ARGMAX) gemv_q8_body<R, MM, decltype(kc)::value>(Q, scale, X, M, N, K, ep);
+  });
+}
+
+template <int R, int MM>
+static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, int M, int N, int K, const Epi& ep,
+                           hipStream_t s) {
+  gemv_q8_kernel<R, MM><<<(N + 4 * R - 1) / (4 * R), 256, 0, s>>>(Q, scale, X, M, N, K, ep);
+}
+
+bool linear_q8_gemv(int M, int K) { return M >= 1 && M <= 8 && K % 16 == 0; }
+
+void launch_quantize_rows(const void* W_bf16, int8_t* Q, float* scale, int N, int K, hipStream_t s) {
+  if (N > 0) quantize_rows_kernel<<<N, 256, 0, s>>>((const bf16*)W_bf16, Q, scale, K);
+}
+
+void launch_dequant_rows(const int8_t* Q, const float* scale, void* out_bf16, int N, int K, hipStream_t s) {
+  const size_t n8 = (size_t)N * K / 8;
+  const int blocks = (int)std::min<size_t>((n8 + 255) / 256, 8192);
+  if (n8) dequant_rows_kernel<<<blocks, 256, 0, s>>>(Q, scale, (bf16*)out_bf16, n8, K);
+}
+
+void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* w_scratch, int M, int N, int K,
+                      const Epi& ep, hipStream_t s) {
+  if (M <= 0) return;
+  if (ep.kind == EPI_ARGMAX) abort();  // the tied lm_head stays bf16
+  const bf16* x = (const bf16*)X;
+  Epi e = ep;
+  e.col_scale = scale;
+  if (linear_q8_gemv(M, K)) {
+    const bool r2 = N >= 8192;
+    if (M <= 1) r2 ? gemv_q8_launch<2, 1>(Q, scale, x, M, N, K, e, s) : gemv_q8_launch<1, 1>(Q, scale, x, M, N, K, e, s);
+    else if (M <= 2) r2 ? gemv_q8_launch<2, 2>(Q, scale, x, M, N, K, e, s) : gemv_q8_launch<1, 2>(Q, scale, x, M, N, K, e, s);
+    else if (M <= 4) r2 ? gemv_q8_launch<2, 4>(Q, scale, x, M, N, K, e, s) : gemv_q8_launch<1, 4>(Q, scale, x, M, N, K, e, s);
+    else gemv_q8_launch<1, 8>(Q, scale, x, M, N, K, e, s);
+    return;
+  }
+  // prefill / wide batches: dequantize to the bf16 scratch, then the bf16 GEMM (or batched GEMV)
+  launch_dequant_rows(Q, nullptr, w_scratch, N, K, s);
+  launch_linear(1, X, w_scratch, M, N, K, e, s);
+}

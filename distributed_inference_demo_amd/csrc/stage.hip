@@ -41,7 +41,10 @@ enum { M_WEMB = 0, M_EMB_G = 1, M_EMB_B = 2, M_LNF_G = 3, M_LNF_B = 4 };
 
 struct Layer {
   void* t[T_NLAYER];
+  float* sc[T_NLAYER];  // int8 stages: per-row scales of the four weight matrices (else null)
 };
+
+static bool is_matrix(int t) { return t == T_QKV_W || t == T_DENSE_W || t == T_FC1_W || t == T_FC2_W; }
 
 struct GraphKey {
   int B, slot, flags;
@@ -73,7 +76,9 @@ constexpr int kSkTickets = 4096;
 struct bs_stage {
   bs_stage_desc d;
   int bf16 = 1;
+  int q8 = 0;              // BS_FLAG_INT8_WEIGHTS: block matrices int8 + row scales
   size_t esz = 2;
+  void* wtmp = nullptr;    // int8 stages: bf16 [4h][h] staging (init) and dequantized operand (prefill)
   int hd = 0, L = 0;
   hipStream_t own = nullptr;
   // HBM
@@ -113,6 +118,7 @@ struct bs_stage {
   unsigned* sk_tickets = nullptr;      // [kSkTickets]
   ProfClass prof;
   std::vector<std::pair<void*, size_t>> order;  // canonical weight order (BS_WEIGHTS_HOST layout)
+  std::vector<std::pair<const float*, int>> order_q8;  // per order entry: (row scales, K) if int8, else (null, 0)
   std::vector<std::pair<GraphKey, hipGraphExec_t>> graphs;  // captured decode steps
   // persistent decode engine (decode_engine.hip): one launch per decode step, B <= 4
   int engine_mode = 0;          // bs_set_engine: 0 auto, 1 launches only, 2 persistent required
@@ -189,6 +195,9 @@ static int validate(const bs_stage_desc* d) {
     return fail(BS_ERR_INVALID, "head vocab slice must be a 16-aligned sub-range of [0, vocab)");
   if (d->weight_source != BS_WEIGHTS_SYNTHETIC && d->weight_source != BS_WEIGHTS_HOST)
     return fail(BS_ERR_INVALID, "unknown weight_source");
+  if (d->flags & ~BS_FLAG_INT8_WEIGHTS) return fail(BS_ERR_INVALID, "unknown desc flags");
+  if ((d->flags & BS_FLAG_INT8_WEIGHTS) && d->dtype != BS_DT_BFLOAT16)
+    return fail(BS_ERR_UNSUPPORTED, "BS_FLAG_INT8_WEIGHTS needs dtype BFLOAT16");
   return BS_OK;
 }
 
@@ -235,6 +244,7 @@ static void free_stage(bs_stage* s) {
   if (s->de_state) hipFree(s->de_state);
   if (s->de_ws) hipFree(s->de_ws);
   if (s->logit_buf) hipFree(s->logit_buf);
+  if (s->wtmp) hipFree(s->wtmp);
   if (s->de_trace) hipFree(s->de_trace);
   if (s->own) hipStreamDestroy(s->own);
   delete s;
@@ -244,7 +254,7 @@ static void free_stage(bs_stage* s) {
 static int engine_init(bs_stage* s) {
   const bs_stage_desc& d = s->d;
   const int h = d.hidden, nh = d.n_head;
-  if (!s->bf16 || h % 512 || h > 4096 || s->L < 1) return BS_OK;   // not eligible: launches only
+  if (!s->bf16 || s->q8 || h % 512 || h > 4096 || s->L < 1) return BS_OK;   // not eligible: launches only
   if (s->kv_half * 2 >= (size_t)0xFFFFFFFFu) return BS_OK;        // 32-bit buffer offsets into one layer's KV
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d.device));
@@ -388,6 +398,7 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   s->d = *desc;
   if (s->d.max_tokens <= 0) s->d.max_tokens = s->d.max_batch * 128;
   s->bf16 = desc->dtype == BS_DT_BFLOAT16;
+  s->q8 = (desc->flags & BS_FLAG_INT8_WEIGHTS) != 0;
   s->esz = s->bf16 ? 2 : 4;
   s->hd = desc->hidden / desc->n_head;
   s->L = desc->layer_end - desc->layer_begin;
@@ -402,12 +413,20 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   size_t off = 0;
   std::vector<size_t> offs;
   auto add = [&](size_t n) { offs.push_back(off); off = align_up(off + n * s->esz, 256); };
+  auto addb = [&](size_t bytes) { offs.push_back(off); off = align_up(off + bytes, 256); };
   if (desc->is_first || desc->is_last) add(V * h);
   if (desc->is_first) { add(h); add(h); }
   size_t lsz[T_NLAYER];
   layer_sizes(h, lsz);
   for (int l = 0; l < s->L; l++)
-    for (int t = 0; t < T_NLAYER; t++) add(lsz[t]);
+    for (int t = 0; t < T_NLAYER; t++) {
+      if (s->q8 && is_matrix(t)) {
+        addb(lsz[t]);                                               // int8 [N][K]
+        addb((t == T_FC1_W ? 4 * h : (t == T_QKV_W ? 3 * h : h)) * 4);  // fp32 scale [N]
+      } else {
+        add(lsz[t]);
+      }
+    }
   if (desc->is_last) { add(h); add(h); }
   const bool slice = desc->head_vocab_end > desc->head_vocab_begin;
   s->hv0 = desc->head_vocab_begin;
@@ -423,7 +442,10 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   if (desc->is_first) { s->emb_g = s->wbase + offs[oi++]; s->emb_b = s->wbase + offs[oi++]; }
   s->layers.resize(s->L);
   for (int l = 0; l < s->L; l++)
-    for (int t = 0; t < T_NLAYER; t++) s->layers[l].t[t] = s->wbase + offs[oi++];
+    for (int t = 0; t < T_NLAYER; t++) {
+      s->layers[l].t[t] = s->wbase + offs[oi++];
+      s->layers[l].sc[t] = (s->q8 && is_matrix(t)) ? (float*)(s->wbase + offs[oi++]) : nullptr;
+    }
   if (desc->is_last) { s->lnf_g = s->wbase + offs[oi++]; s->lnf_b = s->wbase + offs[oi++]; }
   if (slice) {
     if (s->wemb) s->hw = (char*)s->wemb + (size_t)s->hv0 * h * s->esz;
@@ -439,6 +461,20 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   if (desc->is_last) { s->order.push_back({s->lnf_g, h}); s->order.push_back({s->lnf_b, h}); }
   if (slice && !desc->is_first && !desc->is_last) s->order.push_back({s->hw, hrows * h});
   if (slice && !desc->is_last) { s->order.push_back({s->lnf_g, h}); s->order.push_back({s->lnf_b, h}); }
+  s->order_q8.assign(s->order.size(), {nullptr, 0});
+  if (s->q8) {
+    for (size_t i = 0; i < s->order.size(); i++)
+      for (int l = 0; l < s->L; l++)
+        for (int t = 0; t < T_NLAYER; t++)
+          if (s->layers[l].sc[t] && s->order[i].first == s->layers[l].t[t])
+            s->order_q8[i] = {s->layers[l].sc[t], (int)(t == T_FC2_W ? 4 * h : h)};
+    if (hipMalloc(&s->wtmp, 4 * h * h * 2) != hipSuccess) return cleanup(fail(BS_ERR_OOM, "int8 staging allocation failed"));
+  }
+  // int8 matrices are produced in bf16 in the staging buffer, then quantized into the arena
+  auto quantize = [&](size_t i) {
+    const int K = s->order_q8[i].second, N = (int)(s->order[i].second / K);
+    launch_quantize_rows(s->wtmp, (int8_t*)s->order[i].first, (float*)s->order_q8[i].first, N, K, s->own);
+  };
 
   // ---- weights
   if (desc->weight_source == BS_WEIGHTS_SYNTHETIC) {
@@ -447,9 +483,15 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
     if (s->emb_g) launch_gen_fill(s->emb_g, s->bf16, h, tensor_key(seed, -1, M_EMB_G), 2, s->own);
     if (s->emb_b) launch_gen_fill(s->emb_b, s->bf16, h, tensor_key(seed, -1, M_EMB_B), 3, s->own);
     for (int l = 0; l < s->L; l++)
-      for (int t = 0; t < T_NLAYER; t++)
-        launch_gen_fill(s->layers[l].t[t], s->bf16, lsz[t], tensor_key(seed, desc->layer_begin + l, t), layer_kind(t),
-                        s->own);
+      for (int t = 0; t < T_NLAYER; t++) {
+        const bool q = s->layers[l].sc[t] != nullptr;
+        launch_gen_fill(q ? s->wtmp : s->layers[l].t[t], s->bf16, lsz[t], tensor_key(seed, desc->layer_begin + l, t),
+                        layer_kind(t), s->own);
+        if (q) {
+          for (size_t i = 0; i < s->order.size(); i++)
+            if (s->order[i].first == s->layers[l].t[t]) quantize(i);
+        }
+      }
     if (slice && !s->wemb)
       launch_gen_fill(s->hw, s->bf16, hrows * h, tensor_key(seed, -1, M_WEMB), 0, s->own, (uint64_t)s->hv0 * h);
     if (s->lnf_g) launch_gen_fill(s->lnf_g, s->bf16, h, tensor_key(seed, -1, M_LNF_G), 2, s->own);
@@ -463,15 +505,18 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
     float* bounce = nullptr;
     if (hipMalloc(&bounce, chunk * sizeof(float)) != hipSuccess) return cleanup(fail(BS_ERR_OOM, "bounce alloc"));
     const float* src = desc->host_weights;
-    for (auto& o : s->order) {
+    for (size_t oi2 = 0; oi2 < s->order.size(); oi2++) {
+      const auto& o = s->order[oi2];
+      const bool q = s->order_q8[oi2].first != nullptr;
       for (size_t i = 0; i < o.second; i += chunk) {
         const size_t n = std::min(chunk, o.second - i);
         if (hipMemcpyAsync(bounce, src + i, n * sizeof(float), hipMemcpyHostToDevice, s->own) != hipSuccess) {
           hipFree(bounce);
           return cleanup(fail(BS_ERR_DEVICE, "weight upload failed"));
         }
-        launch_convert_f32((char*)o.first + i * s->esz, s->bf16, bounce, n, s->own);
+        launch_convert_f32((char*)(q ? s->wtmp : o.first) + i * s->esz, s->bf16, bounce, n, s->own);
       }
+      if (q) quantize(oi2);
       src += o.second;
     }
     hipStreamSynchronize(s->own);
@@ -561,7 +606,10 @@ extern "C" int bs_read_weights(const bs_stage* s, uint64_t offset, uint64_t coun
   HIP_TRY(hipStreamSynchronize(s->own));
   uint64_t base = 0, done = 0;
   std::vector<uint16_t> tmp;
-  for (const auto& o : s->order) {
+  std::vector<int8_t> qtmp;
+  std::vector<float> stmp;
+  for (size_t oi = 0; oi < s->order.size(); oi++) {
+    const auto& o = s->order[oi];
     const uint64_t b = base, e = base + o.second;
     base = e;
     if (e <= offset || b >= offset + count) continue;
@@ -569,7 +617,15 @@ extern "C" int bs_read_weights(const bs_stage* s, uint64_t offset, uint64_t coun
     const uint64_t n = hi - lo;
     const char* src = (const char*)o.first + (lo - b) * s->esz;
     float* dst = out + (lo - offset);
-    if (s->bf16) {
+    if (s->order_q8[oi].first) {  // int8 matrix: dequantized values Q * scale
+      const int K = s->order_q8[oi].second;
+      const uint64_t r0 = (lo - b) / K, r1 = (hi - b - 1) / K;
+      qtmp.resize(n);
+      stmp.resize(r1 - r0 + 1);
+      HIP_TRY(hipMemcpy(qtmp.data(), (const int8_t*)o.first + (lo - b), n, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(stmp.data(), s->order_q8[oi].first + r0, stmp.size() * 4, hipMemcpyDeviceToHost));
+      for (uint64_t i = 0; i < n; i++) dst[i] = (float)qtmp[i] * stmp[(lo - b + i) / K - r0];
+    } else if (s->bf16) {
       tmp.resize(n);
       HIP_TRY(hipMemcpy(tmp.data(), src, n * 2, hipMemcpyDeviceToHost));
       for (uint64_t i = 0; i < n; i++) {
@@ -716,6 +772,35 @@ static void linear_ln(bs_stage* s, hipStream_t st, const float* x, int row_strid
   }
 }
 
+// Algorithmic bytes of one int8 weight GEMV launch: int8 weights + row scales + bias + activations.
+static double gemv_bytes_q8(const bs_stage* s, int M, int N, int K, int out_bytes) {
+  return (double)N * K + (double)N * 4 + (double)N * s->esz + (double)M * K * s->esz + (double)M * N * out_bytes;
+}
+
+// Block matrix t of a layer: int8 stages stream the int8 weights (launch_linear_q8).
+static void wlinear(bs_stage* s, hipStream_t st, const void* X, const Layer& w, int t, int M, int N, int K,
+                    const Epi& ep, int out_bytes) {
+  if (!w.sc[t]) {
+    linear(s, st, X, w.t[t], M, N, K, ep, out_bytes);
+  } else if (linear_q8_gemv(M, K)) {
+    ProfScope p(s, st, 1, gemv_bytes_q8(s, M, N, K, out_bytes));
+    launch_linear_q8(X, (const int8_t*)w.t[t], w.sc[t], s->wtmp, M, N, K, ep, st);
+  } else {
+    ProfScope p(s, st, 2, 2.0 * M * N * K);
+    launch_linear_q8(X, (const int8_t*)w.t[t], w.sc[t], s->wtmp, M, N, K, ep, st);
+  }
+}
+
+static void wlinear_ln(bs_stage* s, hipStream_t st, const float* x, const void* g, const void* b, const Layer& w,
+                       int t, int M, int N, int K, const Epi& ep, int out_bytes) {
+  if (!w.sc[t]) {
+    linear_ln(s, st, x, 1, 0, g, b, w.t[t], M, N, K, ep, out_bytes);
+    return;
+  }
+  launch_layernorm(1, x, nullptr, 1, 0, g, b, s->xn, 0, M, K, s->d.ln_eps, st);
+  wlinear(s, st, s->xn, w, t, M, N, K, ep, out_bytes);
+}
+
 // Device staging for logits requested with host I/O: one buffer per stage, grown on demand (a
 // stream-ordered hipMallocAsync/hipFreeAsync pair per call handed blocks across the streams of
 // two stages and returned zeros on ROCm 7.2; this is also cheaper).
@@ -770,7 +855,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     e.kind = EPI_QKV; e.bias = w.t[T_QKV_B]; e.q_out = s->q; e.k_cache = kbase; e.v_cache = kbase + s->kv_half;
     e.hidden = h; e.head_dim = hd; e.max_ctx = d.max_ctx; e.n_head = nh; e.seq = S; e.slot = slot; e.past = past;
     e.past_dev = past_dev; e.ldo = 3 * h;
-    linear_ln(s, st, cur, 1, 0, w.t[T_LN1_G], w.t[T_LN1_B], w.t[T_QKV_W], M, 3 * h, h, with_splitk(s, e), 4);
+    wlinear_ln(s, st, cur, w.t[T_LN1_G], w.t[T_LN1_B], w, T_QKV_W, M, 3 * h, h, with_splitk(s, e), 4);
     // attention
     AttnArgs a{};
     a.q = s->q; a.k_cache = kbase; a.v_cache = kbase + s->kv_half; a.ctx_out = s->ctx; a.slopes = s->slopes;
@@ -779,7 +864,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     a.max_chunks = s->max_chunks; a.chunk = s->chunk; a.tickets = s->att_tickets;
     // a split decode context merges in the dense GEMV's prologue when that kernel can take it
     const int nsplit = S == 1 ? attention_decode_splits(B, nh, s->max_chunks) : 1;
-    a.defer_merge = s->bf16 && nsplit > 1 && linear_parts_supported(M, h, hd, nsplit);
+    a.defer_merge = s->bf16 && !s->q8 && nsplit > 1 && linear_parts_supported(M, h, hd, nsplit);
     {
       ProfScope p(s, st, 3, (double)B * nh * (double)(past + S) * hd * 2 * s->esz);
       launch_attention(s->bf16, a, st);
@@ -792,17 +877,17 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
       ProfScope p(s, st, 1, gemv_bytes(s, M, h, h, 4));
       launch_linear_parts(parts, w.t[T_DENSE_W], M, h, h, e2, st);
     } else {
-      linear(s, st, s->ctx, w.t[T_DENSE_W], M, h, h, with_splitk(s, e2), 4);
+      wlinear(s, st, s->ctx, w, T_DENSE_W, M, h, h, with_splitk(s, e2), 4);
     }
     // x2 = LN_post(a); g = gelu(x2 W1 + b1)
     Epi e3{};
     e3.kind = EPI_GELU; e3.bias = w.t[T_FC1_B]; e3.out_act = s->g; e3.ldo = 4 * h;
-    linear_ln(s, st, s->attn, 1, 0, w.t[T_LN2_G], w.t[T_LN2_B], w.t[T_FC1_W], M, 4 * h, h, with_splitk(s, e3), (int)s->esz);
+    wlinear_ln(s, st, s->attn, w.t[T_LN2_G], w.t[T_LN2_B], w, T_FC1_W, M, 4 * h, h, with_splitk(s, e3), (int)s->esz);
     // x = a + g W2 + b2
     float* nxt = (!d.is_last && !host_io && l == s->L - 1) ? (float*)out : (cur == s->xa ? s->xb : s->xa);
     Epi e4{};
     e4.kind = EPI_RESID; e4.bias = w.t[T_FC2_B]; e4.out_f32 = nxt; e4.resid = s->attn; e4.ldo = h;
-    linear(s, st, s->g, w.t[T_FC2_W], M, h, 4 * h, with_splitk(s, e4), 4);
+    wlinear(s, st, s->g, w, T_FC2_W, M, h, 4 * h, with_splitk(s, e4), 4);
     cur = nxt;
   }
 

@@ -37,6 +37,7 @@ BS_WEIGHTS_SYNTHETIC = 0
 BS_WEIGHTS_HOST = 1
 BS_STEP_HOST_IO = 1
 BS_STEP_LOGITS = 2
+BS_FLAG_INT8_WEIGHTS = 1  # bs_stage_desc.flags: weight-only int8 block matrices
 
 DTYPES = {
     1: np.float32, 2: np.uint8, 3: np.int8, 4: np.uint16, 5: np.int16, 6: np.int32, 7: np.int64,
@@ -154,7 +155,7 @@ class Stage:
 
     def __init__(self, hidden, n_head, n_layer, vocab, layer_begin, layer_end, *, dtype="bf16", device=0,
                  max_batch=1, max_ctx=2048, max_tokens=0, seed=0, eps=1e-5, host_weights=None,
-                 is_first=None, is_last=None, head_slice=None):
+                 is_first=None, is_last=None, head_slice=None, int8_weights=False):
         d = StageDesc()
         d.hidden, d.n_head, d.n_layer, d.vocab, d.ln_eps = hidden, n_head, n_layer, vocab, eps
         d.layer_begin, d.layer_end = layer_begin, layer_end
@@ -163,6 +164,7 @@ class Stage:
         d.dtype = BS_DT_BFLOAT16 if dtype in ("bf16", BS_DT_BFLOAT16) else BS_DT_FLOAT
         d.device, d.max_batch, d.max_ctx, d.max_tokens = device, max_batch, max_ctx, max_tokens
         d.seed = seed
+        d.flags = BS_FLAG_INT8_WEIGHTS if int8_weights else 0  # bloom*-int8 variants (server.py:796-799)
         if head_slice is not None:
             d.head_vocab_begin, d.head_vocab_end = head_slice
         self._weights_ref = None

@@ -56,6 +56,14 @@ typedef enum {
   BS_WEIGHTS_HOST = 1       /* fp32 host buffer in canonical stage order (bs_stage_weight_count) */
 } bs_weight_source;
 
+/* desc->flags.  BS_FLAG_INT8_WEIGHTS (bf16 stages): weight-only int8 for the four block matrices
+ * (qkv, dense, fc1, fc2) -- the reference's bloom*-int8 model variants (server.py:796-799,
+ * data/Data.kt:19-30).  Per output row n: scale[n] = max_k |W[n][k]| / 127 (1 for a zero row),
+ * Q[n][k] = round-half-even(W[n][k] / scale[n]) in [-127, 127], W = the bf16 weight.  Embeddings,
+ * LayerNorms, biases and the tied lm_head stay bf16; activations stay bf16/fp32 (weight-only).
+ * bs_read_weights returns Q * scale for the quantized matrices. */
+#define BS_FLAG_INT8_WEIGHTS 1
+
 typedef struct bs_stage_desc {
   /* model (HF BloomConfig fields) */
   int32_t hidden;        /* hidden_size */
@@ -83,7 +91,7 @@ typedef struct bs_stage_desc {
    * (0, 0 = none).  Used by pipelines that spread the tied lm_head over all stages. */
   int32_t head_vocab_begin;
   int32_t head_vocab_end;
-  int32_t flags;         /* reserved, 0 */
+  int32_t flags;         /* BS_FLAG_* (0 = none) */
 } bs_stage_desc;
 
 typedef struct bs_stage bs_stage;

@@ -135,6 +135,41 @@ or_stage *or_create(int hidden, int n_head, int n_layer, int vocab, float eps, i
   return s;
 }
 
+/* ---- Weight-only int8 (the reference's bloom*-int8 variants, server.py:796-799; the rule is
+ * include/bloomstage.h BS_FLAG_INT8_WEIGHTS, whose device side is kernels.hip
+ * quantize_rows_kernel).  The reference's int8 ONNX files come from the absent model_card export
+ * (ORT quantization), so this scheme is the build's own and its parity is against this
+ * restatement only ("parity unpinned" against the reference).  Per output row n of the four
+ * block matrices: scale = max|W[n][:]| / 127 (1 for a zero row), Q = rint(W / scale) clamped to
+ * [-127, 127]; the matrix is replaced by Q * scale (fp32).  Call on a bf16-mode stage. */
+static void quantize_rows(float *W, size_t N, size_t K) {
+#pragma omp parallel for schedule(static)
+  for (size_t n = 0; n < N; n++) {
+    float *w = W + n * K;
+    float amax = 0.f;
+    for (size_t k = 0; k < K; k++) amax = fmaxf(amax, fabsf(w[k]));
+    const float sc = amax > 0.f ? amax / 127.f : 1.f;
+    for (size_t k = 0; k < K; k++) {
+      float q = rintf(w[k] / sc);
+      q = fminf(fmaxf(q, -127.f), 127.f);
+      w[k] = q * sc;
+    }
+  }
+}
+
+int or_quantize_int8(or_stage *s) {
+  if (!s || !s->bf16) return -1;
+  const size_t h = (size_t)s->h;
+  for (int i = 0; i < s->le - s->lb; i++) {
+    or_layer *w = &s->layers[i];
+    quantize_rows(w->qkv_w, 3 * h, h);
+    quantize_rows(w->dense_w, h, h);
+    quantize_rows(w->fc1_w, 4 * h, h);
+    quantize_rows(w->fc2_w, h, 4 * h);
+  }
+  return 0;
+}
+
 void or_destroy(or_stage *s) {
   if (!s) return;
   free(s->wemb); free(s->emb_g); free(s->emb_b); free(s->lnf_g); free(s->lnf_b);

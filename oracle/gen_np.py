@@ -138,3 +138,15 @@ def hf_state_dict(seed: int, hidden: int, n_layer: int, vocab: int, bf16: bool =
             sd[f"transformer.h.{l}.{names[tid]}"] = rnd(tensor(seed, l, tid, shape))
     sd["lm_head.weight"] = sd["transformer.word_embeddings.weight"]
     return sd
+
+
+def int8_rows(w: np.ndarray):
+    """Weight-only int8 rule of BS_FLAG_INT8_WEIGHTS (include/bloomstage.h), numpy restatement of
+    oracle/bloom_oracle.c quantize_rows: per row scale = max|w| / 127 (1 for a zero row),
+    q = rint(w / scale) clamped to [-127, 127].  w: fp32 [N][K] (the bf16-rounded weight).
+    Returns (q int8 [N][K], scale fp32 [N])."""
+    w = np.asarray(w, dtype=np.float32)
+    amax = np.abs(w).max(axis=1)
+    scale = np.where(amax > 0, amax / np.float32(127.0), np.float32(1.0)).astype(np.float32)
+    q = np.clip(np.rint(w / scale[:, None]), -127, 127).astype(np.int8)
+    return q, scale

@@ -28,6 +28,8 @@ def lib():
         L.or_read_kv.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p]
         L.or_num_threads.restype = ctypes.c_int
         L.or_set_accum_double.argtypes = [ctypes.c_int]
+        L.or_quantize_int8.restype = ctypes.c_int
+        L.or_quantize_int8.argtypes = [ctypes.c_void_p]
         L.or_head_norm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.or_head_slice.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -65,7 +67,7 @@ class OracleStage:
     """CPU checker for one pipeline stage; same call semantics as the product Stage."""
 
     def __init__(self, hidden, n_head, n_layer, vocab, layer_begin, layer_end, *, bf16=False,
-                 max_batch=1, max_ctx=64, seed=0, eps=1e-5, is_first=None, is_last=None):
+                 max_batch=1, max_ctx=64, seed=0, eps=1e-5, is_first=None, is_last=None, int8=False):
         self.hidden, self.vocab = hidden, vocab
         self.is_first = layer_begin == 0 if is_first is None else is_first
         self.is_last = layer_end == n_layer if is_last is None else is_last
@@ -73,6 +75,8 @@ class OracleStage:
                                  int(self.is_first), int(self.is_last), int(bf16), max_batch, max_ctx, seed)
         if not self.h:
             raise ValueError("or_create failed (bad stage description)")
+        if int8 and lib().or_quantize_int8(self.h) != 0:  # weight-only int8 (BS_FLAG_INT8_WEIGHTS)
+            raise ValueError("or_quantize_int8 needs a bf16-mode stage")
 
     def forward(self, x, B, S, slot=0, past_len=0, want_logits=False):
         if self.is_first:
