@@ -32,6 +32,8 @@ def parse():
     p.add_argument("--prompt", type=int, default=512)
     p.add_argument("--dtype", default="bf16")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--weights", default="bf16", choices=["bf16", "int8"],
+                   help="int8: weight-only int8 block matrices (BS_FLAG_INT8_WEIGHTS, the bloom*-int8 variants)")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU checker on a bounded sample")
     p.add_argument("--cpu-steps", type=int, default=12)
     p.add_argument("--no-profile", action="store_true")
@@ -60,7 +62,8 @@ def pmc_traffic(args, kernel_tag, timeout=240):
         cmd = [prof, "--pmc", counter, "-d", out, "-o", counter.lower(), "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--steps", "8", "--warmup", "2", "--cpu-baseline", "0",
                "--no-profile", "--no-pmc", "--model", args.model, "--batch", str(args.batch), "--prompt",
-               str(args.prompt), "--dtype", args.dtype, "--seed", str(args.seed), "--engine", args.engine]
+               str(args.prompt), "--dtype", args.dtype, "--seed", str(args.seed), "--engine", args.engine,
+               "--weights", args.weights]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
         except subprocess.TimeoutExpired:
@@ -129,7 +132,7 @@ def bench_single(args):
     dev = torch.device("cuda", 0)
     max_ctx = P + W + K + prof_steps + 1
     st = Stage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, m.n_layer, dtype=args.dtype, device=0, max_batch=B,
-               max_ctx=max_ctx, max_tokens=max(B * P, B), seed=args.seed)
+               max_ctx=max_ctx, max_tokens=max(B * P, B), seed=args.seed, int8_weights=args.weights == "int8")
     wbytes = st.info()["weight_bytes"]
     st.set_engine(args.engine)
     engine = st.engine(B)
@@ -176,6 +179,8 @@ def bench_single(args):
     step_bytes = config.decode_step_bytes(m, m.n_layer, B, ctx_mid, True, True,
                                           w_bytes=2 if args.dtype == "bf16" else 4,
                                           kv_bytes=2 if args.dtype == "bf16" else 4)
+    if args.weights == "int8":  # block matrices: 1 byte per weight + one fp32 scale per output row
+        step_bytes -= m.n_layer * (12.0 * m.hidden * m.hidden * 1 - 9.0 * m.hidden * 4)
     res = {
         "metric": "decode tokens/s, BLOOM pipeline",
         "value": B * K / dt, "unit": "tokens/s", "n_gpus": 1, "steps": K, "warmup": W,
@@ -186,7 +191,7 @@ def bench_single(args):
                                "(BASELINE.json configs[1])",
                    "model": m.name, "stages": 1, "layers_per_stage": [m.n_layer], "batch": B, "prompt": P,
                    "ctx_range": [P + W, P + W + K], "parallelism": "pp1", "weight_bytes": wbytes,
-                   "engine": engine},
+                   "engine": engine, "weights": args.weights},
     }
     if g_n:
         avg_ms = g_ms / g_n
@@ -197,6 +202,8 @@ def bench_single(args):
             unit_note = "algorithmic bytes per launch = the step's weights + K/V read and append + hidden in/out"
         else:
             tag, kname = "gemv", "gemv_rows_kernel (every decode weight GEMV: LN+QKV, dense, LN+fc1, fc2, ln_f+lm_head)"
+            if args.weights == "int8":
+                kname = "gemv_q8_kernel (qkv, dense, fc1, fc2 on int8 weights) + gemv_rows_kernel (ln_f+lm_head, bf16)"
             unit_note = "algorithmic bytes per launch = weights + bias + activations of the GEMV"
         traffic, note = (None, "--no-pmc") if args.no_pmc else pmc_traffic(args, tag)
         res["roofline"] = {"bound": "hbm", "kernel": kname,

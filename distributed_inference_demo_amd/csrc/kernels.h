@@ -114,3 +114,11 @@ bool linear_q8_gemv(int M, int K);
 // dequantized into w_scratch (bf16, N*K) and the bf16 GEMM runs on it.
 void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* w_scratch, int M, int N, int K,
                       const Epi& ep, hipStream_t s);
+// M <= 4, K <= 4096: LayerNorm(x rows) fused into the int8 GEMV prologue (rows normalised to LDS).
+bool linear_q8_ln_fused(int M, int K);
+void launch_linear_q8_ln(const float* x, int row_stride, int row_offset, const void* gamma, const void* beta,
+                         float eps, const int8_t* Q, const float* scale, int M, int N, int K, const Epi& ep,
+                         hipStream_t s);
+// LayerNorm of M fp32 rows -> bf16 (register-resident one-block-per-row kernel when K <= 4096).
+void launch_ln_rows(const float* x, int row_stride, int row_offset, const void* gamma, const void* beta, float eps,
+                    void* out_bf16, int M, int K, hipStream_t s);

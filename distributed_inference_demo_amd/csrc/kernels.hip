@@ -1942,17 +1942,24 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // streams 16 int8 weights (16 B, non-temporal) of each of its rows -- half the bytes of the bf16
 // rows GEMV -- and reads the 16 matching bf16 activations of every row m (L2-resident).  fp32
 // FMAs, DPP wave reduction, the row scale applied once to the reduced sum, then the usual epilogue.
-template <int R, int MM, int KIND>
+template <int R, int MM, bool LN, int KIND>
 __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const float* __restrict__ scale,
-                                             const bf16* __restrict__ X, int M, int N, int K, const Epi& ep) {
+                                             const bf16* __restrict__ Xg, const LnArgs& ln, int M, int N, int K,
+                                             const Epi& ep) {
+  // Offset form: u = q + 128 (one XOR per 4 weights) converts with v_cvt_f32_ubyte{0..3}, one op per
+  // weight; sum_k x*q = sum_k x*u - 128 * sum_k x, the activation sum shared by the R rows.  The
+  // FMAs run on float pairs (v_pk_fma_f32).
+  typedef float f2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
-  const int n0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
-  if (n0 >= N) return;
-  float acc[R][MM];
+  const int n0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;  // waves past N compute row N-1, store nothing
+  f2 acc[R][MM];
+  f2 xs[MM];
 #pragma unroll
-  for (int r = 0; r < R; r++)
+  for (int m = 0; m < MM; m++) {
+    xs[m] = f2{0.f, 0.f};
 #pragma unroll
-    for (int m = 0; m < MM; m++) acc[r][m] = 0.f;
+    for (int r = 0; r < R; r++) acc[r][m] = f2{0.f, 0.f};
+  }
   const int8_t* wr[R];
 #pragma unroll
   for (int r = 0; r < R; r++) wr[r] = Q + (size_t)min(n0 + r, N - 1) * K;
@@ -1962,6 +1969,18 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
 #pragma unroll
     for (int r = 0; r < R; r++) wv[r] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c));
   }
+  // LN: the block normalises its M fp32 rows into LDS while the first weight loads fly
+  extern __shared__ __align__(16) unsigned char q8_lds[];
+  const bf16* X = Xg;
+  if constexpr (LN) {
+    __shared__ float scratch[64];
+    float4 xv[MM][4];
+    float cc[MM];
+    uint2 gb[4][2];
+    ln_rows_load<MM>(ln, M, K, xv, cc, gb);
+    ln_rows_finish<MM>(ln, M, K, xv, cc, gb, reinterpret_cast<bf16*>(q8_lds), scratch);
+    X = reinterpret_cast<const bf16*>(q8_lds);
+  }
   for (; c < K; c += 1024) {
     i32x4 cur[R];
 #pragma unroll
@@ -1970,24 +1989,33 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
 #pragma unroll
       for (int r = 0; r < R; r++) wv[r] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c + 1024));
     }
-    float wf[R][16];
+    f2 wf[R][8];
 #pragma unroll
     for (int r = 0; r < R; r++)
 #pragma unroll
-      for (int j = 0; j < 16; j++) wf[r][j] = (float)((cur[r][j >> 2] << (24 - 8 * (j & 3))) >> 24);
+      for (int i = 0; i < 4; i++) {
+        const uint32_t u = (uint32_t)cur[r][i] ^ 0x80808080u;
+        wf[r][2 * i] = f2{(float)(u & 0xFF), (float)((u >> 8) & 0xFF)};
+        wf[r][2 * i + 1] = f2{(float)((u >> 16) & 0xFF), (float)(u >> 24)};
+      }
 #pragma unroll
     for (int m = 0; m < MM; m++) {
       if (m < M) {
-        u16x8 a0, a1;
-        raw_load(X + (size_t)m * K + c, a0);
-        raw_load(X + (size_t)m * K + c + 8, a1);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 a0 = *reinterpret_cast<const u32x4*>(X + (size_t)m * K + c);
+        const u32x4 a1 = *reinterpret_cast<const u32x4*>(X + (size_t)m * K + c + 8);
+        f2 xf[8];
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-#pragma unroll
-          for (int j = 0; j < 8; j++) acc[r][m] = fmaf(raw_get(a0, j), wf[r][j], acc[r][m]);
-#pragma unroll
-          for (int j = 0; j < 8; j++) acc[r][m] = fmaf(raw_get(a1, j), wf[r][8 + j], acc[r][m]);
+        for (int i = 0; i < 4; i++) {
+          xf[i] = f2{__uint_as_float(a0[i] << 16), __uint_as_float(a0[i] & 0xFFFF0000u)};
+          xf[4 + i] = f2{__uint_as_float(a1[i] << 16), __uint_as_float(a1[i] & 0xFFFF0000u)};
         }
+#pragma unroll
+        for (int i = 0; i < 8; i++) xs[m] += xf[i];
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+          for (int i = 0; i < 8; i++) acc[r][m] = __builtin_elementwise_fma(xf[i], wf[r][i], acc[r][m]);
       }
     }
   }
@@ -1997,7 +2025,7 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
 #pragma unroll
     for (int m = 0; m < MM; m++) {
       if (m < M) {
-        const float t = wave_sum(acc[r][m]);
+        const float t = wave_sum((acc[r][m].x + acc[r][m].y) - 128.f * (xs[m].x + xs[m].y));
         if (lane == r * MM + m) mine = t;
       }
     }
@@ -2005,21 +2033,39 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
   if (lane < R * MM && m < M && n0 + r < N) epi_store<bf16, KIND>(ep, m, n0 + r, mine);  // ep.col_scale = scale
 }
 
-template <int R, int MM>
+template <int R, int MM, bool LN>
 __global__ __launch_bounds__(256) void gemv_q8_kernel(const int8_t* __restrict__ Q, const float* __restrict__ scale,
-                                                      const bf16* __restrict__ X, int M, int N, int K, Epi ep) {
+                                                      const bf16* __restrict__ X, LnArgs ln, int M, int N, int K, Epi ep) {
   epi_dispatch(ep.kind, [&](auto kc) {
-    if constexpr (decltype(kc)::value != EPI_ARGMAX) gemv_q8_body<R, MM, decltype(kc)::value>(Q, scale, X, M, N, K, ep);
+    if constexpr (decltype(kc)::value != EPI_ARGMAX)
+      gemv_q8_body<R, MM, LN, decltype(kc)::value>(Q, scale, X, ln, M, N, K, ep);
   });
 }
 
-template <int R, int MM>
-static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, int M, int N, int K, const Epi& ep,
-                           hipStream_t s) {
-  gemv_q8_kernel<R, MM><<<(N + 4 * R - 1) / (4 * R), 256, 0, s>>>(Q, scale, X, M, N, K, ep);
+template <int R, int MM, bool LN = false>
+static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, const LnArgs& ln, int M, int N, int K,
+                           const Epi& ep, hipStream_t s) {
+  const size_t shm = LN ? (size_t)M * K * sizeof(bf16) : 0;
+  gemv_q8_kernel<R, MM, LN><<<(N + 4 * R - 1) / (4 * R), 256, shm, s>>>(Q, scale, X, ln, M, N, K, ep);
 }
 
 bool linear_q8_gemv(int M, int K) { return M >= 1 && M <= 8 && K % 16 == 0; }
+bool linear_q8_ln_fused(int M, int K) { return M >= 1 && M <= 4 && K % 16 == 0 && K <= 4096; }
+
+void launch_linear_q8_ln(const float* x, int row_stride, int row_offset, const void* gamma, const void* beta,
+                         float eps, const int8_t* Q, const float* scale, int M, int N, int K, const Epi& ep,
+                         hipStream_t s) {
+  Epi e = ep;
+  e.col_scale = scale;
+  const LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
+  const bool r2 = N >= 8192;
+  if (M <= 1) r2 ? gemv_q8_launch<2, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s)
+              : gemv_q8_launch<1, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s);
+  else if (M <= 2) r2 ? gemv_q8_launch<2, 2, true>(Q, scale, nullptr, ln, M, N, K, e, s)
+                   : gemv_q8_launch<1, 2, true>(Q, scale, nullptr, ln, M, N, K, e, s);
+  else r2 ? gemv_q8_launch<2, 4, true>(Q, scale, nullptr, ln, M, N, K, e, s)
+          : gemv_q8_launch<1, 4, true>(Q, scale, nullptr, ln, M, N, K, e, s);
+}
 
 void launch_quantize_rows(const void* W_bf16, int8_t* Q, float* scale, int N, int K, hipStream_t s) {
   if (N > 0) quantize_rows_kernel<<<N, 256, 0, s>>>((const bf16*)W_bf16, Q, scale, K);
@@ -2031,6 +2077,16 @@ void launch_dequant_rows(const int8_t* Q, const float* scale, void* out_bf16, in
   if (n8) dequant_rows_kernel<<<blocks, 256, 0, s>>>(Q, scale, (bf16*)out_bf16, n8, K);
 }
 
+void launch_ln_rows(const float* x, int row_stride, int row_offset, const void* gamma, const void* beta, float eps,
+                    void* out_bf16, int M, int K, hipStream_t s) {
+  if (K <= 4096 && (K % 4) == 0) {
+    LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
+    ln_rows_kernel<<<M, 256, 0, s>>>(ln, K, (bf16*)out_bf16);
+  } else {
+    launch_layernorm(1, x, nullptr, row_stride, row_offset, gamma, beta, out_bf16, 0, M, K, eps, s);
+  }
+}
+
 void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* w_scratch, int M, int N, int K,
                       const Epi& ep, hipStream_t s) {
   if (M <= 0) return;
@@ -2040,10 +2096,11 @@ void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* 
   e.col_scale = scale;
   if (linear_q8_gemv(M, K)) {
     const bool r2 = N >= 8192;
-    if (M <= 1) r2 ? gemv_q8_launch<2, 1>(Q, scale, x, M, N, K, e, s) : gemv_q8_launch<1, 1>(Q, scale, x, M, N, K, e, s);
-    else if (M <= 2) r2 ? gemv_q8_launch<2, 2>(Q, scale, x, M, N, K, e, s) : gemv_q8_launch<1, 2>(Q, scale, x, M, N, K, e, s);
-    else if (M <= 4) r2 ? gemv_q8_launch<2, 4>(Q, scale, x, M, N, K, e, s) : gemv_q8_launch<1, 4>(Q, scale, x, M, N, K, e, s);
-    else gemv_q8_launch<1, 8>(Q, scale, x, M, N, K, e, s);
+    const LnArgs ln{};
+    if (M <= 1) r2 ? gemv_q8_launch<2, 1>(Q, scale, x, ln, M, N, K, e, s) : gemv_q8_launch<1, 1>(Q, scale, x, ln, M, N, K, e, s);
+    else if (M <= 2) r2 ? gemv_q8_launch<2, 2>(Q, scale, x, ln, M, N, K, e, s) : gemv_q8_launch<1, 2>(Q, scale, x, ln, M, N, K, e, s);
+    else if (M <= 4) r2 ? gemv_q8_launch<2, 4>(Q, scale, x, ln, M, N, K, e, s) : gemv_q8_launch<1, 4>(Q, scale, x, ln, M, N, K, e, s);
+    else gemv_q8_launch<1, 8>(Q, scale, x, ln, M, N, K, e, s);
     return;
   }
   // prefill / wide batches: dequantize to the bf16 scratch, then the bf16 GEMM (or batched GEMV)

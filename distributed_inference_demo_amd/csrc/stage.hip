@@ -797,7 +797,12 @@ static void wlinear_ln(bs_stage* s, hipStream_t st, const float* x, const void* 
     linear_ln(s, st, x, 1, 0, g, b, w.t[t], M, N, K, ep, out_bytes);
     return;
   }
-  launch_layernorm(1, x, nullptr, 1, 0, g, b, s->xn, 0, M, K, s->d.ln_eps, st);
+  if (linear_q8_ln_fused(M, K)) {
+    ProfScope p(s, st, 1, gemv_bytes_q8(s, M, N, K, out_bytes));
+    launch_linear_q8_ln(x, 1, 0, g, b, s->d.ln_eps, (const int8_t*)w.t[t], w.sc[t], M, N, K, ep, st);
+    return;
+  }
+  launch_ln_rows(x, 1, 0, g, b, s->d.ln_eps, s->xn, M, K, st);
   wlinear(s, st, s->xn, w, t, M, N, K, ep, out_bytes);
 }
 
