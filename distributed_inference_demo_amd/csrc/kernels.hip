@@ -2050,6 +2050,16 @@ static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, c
 }
 
 bool linear_q8_gemv(int M, int K) { return M >= 1 && M <= 8 && K % 16 == 0; }
+
+// Rows per wave of the int8 GEMV: 2 (profiles/r01_q8_rows_sweep.txt: 1b1 B=1 1128 -> 1177 tok/s against 1 row
+// below N = 8192, 7b1 equal); BS_Q8_R=1|2|4 forces it (4 only at M = 1).
+static int q8_rows(int N) {
+  static const int forced = [] {
+    const char* e = getenv("BS_Q8_R");
+    return e && *e ? atoi(e) : 0;
+  }();
+  return forced ? forced : 2;
+}
 bool linear_q8_ln_fused(int M, int K) { return M >= 1 && M <= 4 && K % 16 == 0 && K <= 4096; }
 
 void launch_linear_q8_ln(const float* x, int row_stride, int row_offset, const void* gamma, const void* beta,
@@ -2058,9 +2068,11 @@ void launch_linear_q8_ln(const float* x, int row_stride, int row_offset, const v
   Epi e = ep;
   e.col_scale = scale;
   const LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
-  const bool r2 = N >= 8192;
-  if (M <= 1) r2 ? gemv_q8_launch<2, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s)
-              : gemv_q8_launch<1, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s);
+  const int rr = q8_rows(N);
+  const bool r2 = rr >= 2;
+  if (M <= 1 && rr == 4) gemv_q8_launch<4, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s);
+  else if (M <= 1) r2 ? gemv_q8_launch<2, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s)
+                   : gemv_q8_launch<1, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s);
   else if (M <= 2) r2 ? gemv_q8_launch<2, 2, true>(Q, scale, nullptr, ln, M, N, K, e, s)
                    : gemv_q8_launch<1, 2, true>(Q, scale, nullptr, ln, M, N, K, e, s);
   else r2 ? gemv_q8_launch<2, 4, true>(Q, scale, nullptr, ln, M, N, K, e, s)
@@ -2095,9 +2107,11 @@ void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* 
   Epi e = ep;
   e.col_scale = scale;
   if (linear_q8_gemv(M, K)) {
-    const bool r2 = N >= 8192;
+    const int rr = q8_rows(N);
+    const bool r2 = rr >= 2;
     const LnArgs ln{};
-    if (M <= 1) r2 ? gemv_q8_launch<2, 1>(Q, scale, x, ln, M, N, K, e, s) : gemv_q8_launch<1, 1>(Q, scale, x, ln, M, N, K, e, s);
+    if (M <= 1 && rr == 4) gemv_q8_launch<4, 1>(Q, scale, x, ln, M, N, K, e, s);
+    else if (M <= 1) r2 ? gemv_q8_launch<2, 1>(Q, scale, x, ln, M, N, K, e, s) : gemv_q8_launch<1, 1>(Q, scale, x, ln, M, N, K, e, s);
     else if (M <= 2) r2 ? gemv_q8_launch<2, 2>(Q, scale, x, ln, M, N, K, e, s) : gemv_q8_launch<1, 2>(Q, scale, x, ln, M, N, K, e, s);
     else if (M <= 4) r2 ? gemv_q8_launch<2, 4>(Q, scale, x, ln, M, N, K, e, s) : gemv_q8_launch<1, 4>(Q, scale, x, ln, M, N, K, e, s);
     else gemv_q8_launch<1, 8>(Q, scale, x, ln, M, N, K, e, s);
