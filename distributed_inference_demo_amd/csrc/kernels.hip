@@ -1942,7 +1942,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // streams 16 int8 weights (16 B, non-temporal) of each of its rows -- half the bytes of the bf16
 // rows GEMV -- and reads the 16 matching bf16 activations of every row m (L2-resident).  fp32
 // FMAs, DPP wave reduction, the row scale applied once to the reduced sum, then the usual epilogue.
-template <int R, int MM, bool LN, int KIND>
+template <int R, int MM, bool LN, int KIND, int CW>
 __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const float* __restrict__ scale,
                                              const bf16* __restrict__ Xg, const LnArgs& ln, int M, int N, int K,
                                              const Epi& ep) {
@@ -1963,11 +1963,16 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
   const int8_t* wr[R];
 #pragma unroll
   for (int r = 0; r < R; r++) wr[r] = Q + (size_t)min(n0 + r, N - 1) * K;
-  int c = lane * 16;
-  i32x4 wv[R];
+  // CW bytes of each row per lane per step (16 or 32): the next step's R x CW bytes are in flight
+  // during this step's FMAs
+  constexpr int W = CW / 16, STEP = 64 * CW;
+  int c = lane * CW;
+  i32x4 wv[R][W];
   if (c < K) {
 #pragma unroll
-    for (int r = 0; r < R; r++) wv[r] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c));
+    for (int r = 0; r < R; r++)
+#pragma unroll
+      for (int w = 0; w < W; w++) wv[r][w] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c + 16 * w));
   }
   // LN: the block normalises its M fp32 rows into LDS while the first weight loads fly
   extern __shared__ __align__(16) unsigned char q8_lds[];
@@ -1981,41 +1986,50 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
     ln_rows_finish<MM>(ln, M, K, xv, cc, gb, reinterpret_cast<bf16*>(q8_lds), scratch);
     X = reinterpret_cast<const bf16*>(q8_lds);
   }
-  for (; c < K; c += 1024) {
-    i32x4 cur[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) cur[r] = wv[r];
-    if (c + 1024 < K) {  // next step's weights in flight during this step's FMAs
-#pragma unroll
-      for (int r = 0; r < R; r++) wv[r] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c + 1024));
-    }
-    f2 wf[R][8];
+  for (; c < K; c += STEP) {
+    i32x4 cur[R][W];
 #pragma unroll
     for (int r = 0; r < R; r++)
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t u = (uint32_t)cur[r][i] ^ 0x80808080u;
-        wf[r][2 * i] = f2{(float)(u & 0xFF), (float)((u >> 8) & 0xFF)};
-        wf[r][2 * i + 1] = f2{(float)((u >> 16) & 0xFF), (float)(u >> 24)};
-      }
+      for (int w = 0; w < W; w++) cur[r][w] = wv[r][w];
+    if (c + STEP < K) {
 #pragma unroll
-    for (int m = 0; m < MM; m++) {
-      if (m < M) {
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 a0 = *reinterpret_cast<const u32x4*>(X + (size_t)m * K + c);
-        const u32x4 a1 = *reinterpret_cast<const u32x4*>(X + (size_t)m * K + c + 8);
-        f2 xf[8];
+      for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int w = 0; w < W; w++)
+          wv[r][w] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c + STEP + 16 * w));
+    }
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int cw = c + 16 * w;
+      f2 wf[R][8];
+#pragma unroll
+      for (int r = 0; r < R; r++)
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-          xf[i] = f2{__uint_as_float(a0[i] << 16), __uint_as_float(a0[i] & 0xFFFF0000u)};
-          xf[4 + i] = f2{__uint_as_float(a1[i] << 16), __uint_as_float(a1[i] & 0xFFFF0000u)};
+          const uint32_t u = (uint32_t)cur[r][w][i] ^ 0x80808080u;
+          wf[r][2 * i] = f2{(float)(u & 0xFF), (float)((u >> 8) & 0xFF)};
+          wf[r][2 * i + 1] = f2{(float)((u >> 16) & 0xFF), (float)(u >> 24)};
         }
 #pragma unroll
-        for (int i = 0; i < 8; i++) xs[m] += xf[i];
+      for (int m = 0; m < MM; m++) {
+        if (m < M) {
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 a0 = *reinterpret_cast<const u32x4*>(X + (size_t)m * K + cw);
+          const u32x4 a1 = *reinterpret_cast<const u32x4*>(X + (size_t)m * K + cw + 8);
+          f2 xf[8];
 #pragma unroll
-        for (int r = 0; r < R; r++)
+          for (int i = 0; i < 4; i++) {
+            xf[i] = f2{__uint_as_float(a0[i] << 16), __uint_as_float(a0[i] & 0xFFFF0000u)};
+            xf[4 + i] = f2{__uint_as_float(a1[i] << 16), __uint_as_float(a1[i] & 0xFFFF0000u)};
+          }
 #pragma unroll
-          for (int i = 0; i < 8; i++) acc[r][m] = __builtin_elementwise_fma(xf[i], wf[r][i], acc[r][m]);
+          for (int i = 0; i < 8; i++) xs[m] += xf[i];
+#pragma unroll
+          for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int i = 0; i < 8; i++) acc[r][m] = __builtin_elementwise_fma(xf[i], wf[r][i], acc[r][m]);
+        }
       }
     }
   }
@@ -2033,23 +2047,34 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
   if (lane < R * MM && m < M && n0 + r < N) epi_store<bf16, KIND>(ep, m, n0 + r, mine);  // ep.col_scale = scale
 }
 
-template <int R, int MM, bool LN>
+template <int R, int MM, bool LN, int CW>
 __global__ __launch_bounds__(256) void gemv_q8_kernel(const int8_t* __restrict__ Q, const float* __restrict__ scale,
                                                       const bf16* __restrict__ X, LnArgs ln, int M, int N, int K, Epi ep) {
   epi_dispatch(ep.kind, [&](auto kc) {
     if constexpr (decltype(kc)::value != EPI_ARGMAX)
-      gemv_q8_body<R, MM, LN, decltype(kc)::value>(Q, scale, X, ln, M, N, K, ep);
+      gemv_q8_body<R, MM, LN, decltype(kc)::value, CW>(Q, scale, X, ln, M, N, K, ep);
   });
+}
+
+// Bytes per lane per weight row and step: BS_Q8_CW=16|32 (A/B knob), default 16.
+static int q8_cw() {
+  static const int v = [] {
+    const char* e = getenv("BS_Q8_CW");
+    return e && atoi(e) == 32 ? 32 : 16;
+  }();
+  return v;
 }
 
 template <int R, int MM, bool LN = false>
 static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, const LnArgs& ln, int M, int N, int K,
                            const Epi& ep, hipStream_t s) {
   const size_t shm = LN ? (size_t)M * K * sizeof(bf16) : 0;
-  gemv_q8_kernel<R, MM, LN><<<(N + 4 * R - 1) / (4 * R), 256, shm, s>>>(Q, scale, X, ln, M, N, K, ep);
+  const int blocks = (N + 4 * R - 1) / (4 * R);
+  if (q8_cw() == 32) gemv_q8_kernel<R, MM, LN, 32><<<blocks, 256, shm, s>>>(Q, scale, X, ln, M, N, K, ep);
+  else gemv_q8_kernel<R, MM, LN, 16><<<blocks, 256, shm, s>>>(Q, scale, X, ln, M, N, K, ep);
 }
 
-bool linear_q8_gemv(int M, int K) { return M >= 1 && M <= 8 && K % 16 == 0; }
+bool linear_q8_gemv(int M, int K) { return M >= 1 && M <= 8 && K % 32 == 0; }
 
 // Rows per wave of the int8 GEMV: 2 (profiles/r01_q8_rows_sweep.txt: 1b1 B=1 1128 -> 1177 tok/s against 1 row
 // below N = 8192, 7b1 equal); BS_Q8_R=1|2|4 forces it (4 only at M = 1).
@@ -2060,7 +2085,7 @@ static int q8_rows(int N) {
   }();
   return forced ? forced : 2;
 }
-bool linear_q8_ln_fused(int M, int K) { return M >= 1 && M <= 4 && K % 16 == 0 && K <= 4096; }
+bool linear_q8_ln_fused(int M, int K) { return M >= 1 && M <= 4 && K % 32 == 0 && K <= 4096; }
 
 void launch_linear_q8_ln(const float* x, int row_stride, int row_offset, const void* gamma, const void* beta,
                          float eps, const int8_t* Q, const float* scale, int M, int N, int K, const Epi& ep,
