@@ -126,13 +126,16 @@ def bench_single(args):
     from distributed_inference_demo_amd.stage import Stage
 
     m = config.get(args.model)
+    if m.int8_weights:  # "-int8" model name
+        args.weights = "int8"
     B, P, K, W = args.batch, args.prompt, args.steps, args.warmup
     prof_steps = 0 if args.no_profile else min(16, K)
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     max_ctx = P + W + K + prof_steps + 1
     st = Stage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, m.n_layer, dtype=args.dtype, device=0, max_batch=B,
-               max_ctx=max_ctx, max_tokens=max(B * P, B), seed=args.seed, int8_weights=args.weights == "int8")
+               max_ctx=max_ctx, max_tokens=max(B * P, B), seed=args.seed,
+               int8_weights=args.weights == "int8" or m.int8_weights)
     wbytes = st.info()["weight_bytes"]
     st.set_engine(args.engine)
     engine = st.engine(B)

@@ -1,6 +1,6 @@
 """BLOOM family dimensions (HF BloomConfig fields; SURVEY.md §8 model table) and the
 benchmark configurations of BASELINE.json."""
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 
 
 @dataclass(frozen=True)
@@ -11,6 +11,7 @@ class BloomDims:
     n_head: int
     vocab: int = 250880
     eps: float = 1e-5
+    int8_weights: bool = False  # "-int8" model names: weight-only int8 stages (BS_FLAG_INT8_WEIGHTS)
 
     @property
     def head_dim(self):
@@ -32,8 +33,15 @@ MODELS = {
 
 
 def get(name: str) -> BloomDims:
-    key = name if name.startswith("bloom-") or name in MODELS else f"bloom-{name}"
-    return MODELS[key]
+    """Model by name: "bloom-560m", "560m", the reference's "bloom560m"; an "-int8" suffix
+    ("bloom560m-int8", server.py:796-799) selects the weight-only int8 variant of the same dims."""
+    int8 = name.endswith("-int8")
+    base = name[:-5] if int8 else name
+    if base.startswith("bloom") and not base.startswith("bloom-") and base not in MODELS:
+        base = "bloom-" + base[5:]
+    key = base if base.startswith("bloom-") or base in MODELS else f"bloom-{base}"
+    m = MODELS[key]
+    return replace(m, name=m.name + "-int8", int8_weights=True) if int8 else m
 
 
 def decode_step_bytes(m: BloomDims, layers: int, batch: int, ctx: int, first: bool, last: bool,

@@ -241,7 +241,8 @@ def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb
         st = Stage(model.hidden, model.n_head, model.n_layer, model.vocab, lb, le, dtype=dtype,
                    device=device.index if device.type == "cuda" else 0, max_batch=mb_rows * n_mb,
                    max_ctx=max_ctx, max_tokens=mb_rows * max_seq, seed=seed, is_first=is_first,
-                   is_last=is_last and not head_split, head_slice=hslice)
+                   is_last=is_last and not head_split, head_slice=hslice,
+                   int8_weights=model.int8_weights and dtype == "bf16")
         ex = StageExecutor(st)
     else:
         ex = executor_factory(lb, le, is_first, is_last and not head_split, mb_rows * n_mb, max_ctx, hslice)
@@ -262,6 +263,8 @@ def bench_pipeline(args):
     rank, world, local = init_distributed("nccl")
     dev = torch.device("cuda", local)
     model = config.get(args.model)
+    if getattr(args, "weights", "bf16") == "int8":
+        model = config.get(model.name if model.int8_weights else model.name + "-int8")
     B, P, K, W = args.batch, args.prompt, args.steps, args.warmup
     head_split = not getattr(args, "no_head_split", False)
     pipe, (lb, le) = build_rank(model, rank, world, dev, dtype=args.dtype, mb_rows=B, max_ctx=P + W + K + 2,

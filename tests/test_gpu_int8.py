@@ -118,3 +118,26 @@ def test_int8_long_context_graph_decode():
             if step % 5 == 0 or step == 23:
                 torch.cuda.synchronize()
                 check_close(lg.cpu().numpy(), lo, "bf16", f"int8 graph decode step {step}")
+
+
+def test_serve_run_int8_on_gpu_matches_oracle():
+    """serve.py lifecycle on one GPU with an int8 model (bf16 stage, BS_FLAG_INT8_WEIGHTS): 4 samples,
+    2 in flight; each sample's greedy ids against the int8 oracle decoding it alone (bf16 noise may
+    flip a near-tie later in a sequence: the first id must match, 80 % of all ids)."""
+    import torch
+    from distributed_inference_demo_amd.config import BloomDims
+    from distributed_inference_demo_amd.serve import RunConfig, run_rank, synthetic_prompts
+    model = BloomDims("tinygpu-int8", 256, 2, 4, vocab=1024, int8_weights=True)
+    cfg = RunConfig(model=model, num_sample=4, max_length=8, core_pool_size=2, prompt_len=9, dtype="bf16", seed=13)
+    res = run_rank(cfg, 0, 1, torch.device("cuda", 0))
+    agree = []
+    for got, p in zip(res["samples"], synthetic_prompts(cfg, model.vocab)):
+        o = OracleStage(256, 4, 2, 1024, 0, 2, bf16=True, max_batch=1, max_ctx=32, seed=13, int8=True)
+        tok = o.forward(np.array(p, np.int32).reshape(1, -1), 1, len(p))
+        ids = [int(tok[0])]
+        for i in range(cfg.max_length - 1):
+            tok = o.forward(np.array([[got[i]]], np.int32), 1, 1, past_len=len(p) + i)  # teacher-forced
+            ids.append(int(tok[0]))
+        assert got[0] == ids[0]
+        agree += [a == b for a, b in zip(got, ids)]
+    assert np.mean(agree) >= 0.8

@@ -39,3 +39,12 @@ def test_oracle_int8_needs_bf16_mode():
 def test_int8_flag_rejected_on_fp32_stage():
     with pytest.raises(BloomStageError, match="BFLOAT16"):
         Stage(64, 4, 1, 256, 0, 1, dtype="fp32", max_ctx=4, int8_weights=True)
+
+
+def test_int8_model_names():
+    """The reference's model request names (server.py:796-799): "bloom560m" / "bloom560m-int8"."""
+    from distributed_inference_demo_amd import config
+    a, b = config.get("bloom560m"), config.get("bloom560m-int8")
+    assert (a.name, a.int8_weights) == ("bloom-560m", False)
+    assert (b.name, b.int8_weights, b.hidden, b.n_layer) == ("bloom-560m-int8", True, 1024, 24)
+    assert config.get("bloom-7b1-int8").int8_weights and not config.get("7b1").int8_weights
