@@ -1942,7 +1942,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // streams 16 int8 weights (16 B, non-temporal) of each of its rows -- half the bytes of the bf16
 // rows GEMV -- and reads the 16 matching bf16 activations of every row m (L2-resident).  fp32
 // FMAs, DPP wave reduction, the row scale applied once to the reduced sum, then the usual epilogue.
-template <int R, int MM, bool LN, int KIND, int CW>
+template <int R, int MM, bool LN, int KIND, int CW, bool XL>
 __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const float* __restrict__ scale,
                                              const bf16* __restrict__ Xg, const LnArgs& ln, int M, int N, int K,
                                              const Epi& ep) {
@@ -1984,6 +1984,12 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
     uint2 gb[4][2];
     ln_rows_load<MM>(ln, M, K, xv, cc, gb);
     ln_rows_finish<MM>(ln, M, K, xv, cc, gb, reinterpret_cast<bf16*>(q8_lds), scratch);
+    X = reinterpret_cast<const bf16*>(q8_lds);
+  } else if (XL) {  // plain X staged once per block in LDS (the 4 waves share it; one L2 pass)
+    const int n16 = M * K / 8;
+    for (int i = threadIdx.x; i < n16; i += 256)
+      reinterpret_cast<u16x8*>(q8_lds)[i] = reinterpret_cast<const u16x8*>(Xg)[i];
+    __syncthreads();
     X = reinterpret_cast<const bf16*>(q8_lds);
   }
   for (; c < K; c += STEP) {
@@ -2047,12 +2053,12 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
   if (lane < R * MM && m < M && n0 + r < N) epi_store<bf16, KIND>(ep, m, n0 + r, mine);  // ep.col_scale = scale
 }
 
-template <int R, int MM, bool LN, int CW>
+template <int R, int MM, bool LN, int CW, bool XL = false>
 __global__ __launch_bounds__(256) void gemv_q8_kernel(const int8_t* __restrict__ Q, const float* __restrict__ scale,
                                                       const bf16* __restrict__ X, LnArgs ln, int M, int N, int K, Epi ep) {
   epi_dispatch(ep.kind, [&](auto kc) {
     if constexpr (decltype(kc)::value != EPI_ARGMAX)
-      gemv_q8_body<R, MM, LN, decltype(kc)::value, CW>(Q, scale, X, ln, M, N, K, ep);
+      gemv_q8_body<R, MM, LN, decltype(kc)::value, CW, XL>(Q, scale, X, ln, M, N, K, ep);
   });
 }
 
@@ -2068,8 +2074,19 @@ static int q8_cw() {
 template <int R, int MM, bool LN = false>
 static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, const LnArgs& ln, int M, int N, int K,
                            const Epi& ep, hipStream_t s) {
-  const size_t shm = LN ? (size_t)M * K * sizeof(bf16) : 0;
+  static const bool xl = [] {  // BS_Q8_XL=1: plain X staged in LDS when it fits 64 KB (A/B knob)
+    const char* e = getenv("BS_Q8_XL");
+    return e && *e == '1';
+  }();
+  const bool stage_x = !LN && xl && (size_t)M * K * sizeof(bf16) <= 65536;
+  const size_t shm = (LN || stage_x) ? (size_t)M * K * sizeof(bf16) : 0;
   const int blocks = (N + 4 * R - 1) / (4 * R);
+  if constexpr (!LN) {
+    if (stage_x) {
+      gemv_q8_kernel<R, MM, false, 16, true><<<blocks, 256, shm, s>>>(Q, scale, X, ln, M, N, K, ep);
+      return;
+    }
+  }
   if (q8_cw() == 32) gemv_q8_kernel<R, MM, LN, 32><<<blocks, 256, shm, s>>>(Q, scale, X, ln, M, N, K, ep);
   else gemv_q8_kernel<R, MM, LN, 16><<<blocks, 256, shm, s>>>(Q, scale, X, ln, M, N, K, ep);
 }
