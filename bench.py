@@ -39,8 +39,6 @@ def parse():
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     p.add_argument("--no-head-split", action="store_true", help="pipeline: keep the whole lm_head on the last stage")
-    p.add_argument("--engine", default="auto", choices=["auto", "launches", "persistent"],
-                   help="decode engine (bs_set_engine): auto = one persistent launch per step when eligible")
     return p.parse_args()
 
 
@@ -62,7 +60,7 @@ def pmc_traffic(args, kernel_tag, timeout=240):
         cmd = [prof, "--pmc", counter, "-d", out, "-o", counter.lower(), "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--steps", "8", "--warmup", "2", "--cpu-baseline", "0",
                "--no-profile", "--no-pmc", "--model", args.model, "--batch", str(args.batch), "--prompt",
-               str(args.prompt), "--dtype", args.dtype, "--seed", str(args.seed), "--engine", args.engine,
+               str(args.prompt), "--dtype", args.dtype, "--seed", str(args.seed),
                "--weights", args.weights]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
@@ -137,8 +135,6 @@ def bench_single(args):
                max_ctx=max_ctx, max_tokens=max(B * P, B), seed=args.seed,
                int8_weights=args.weights == "int8" or m.int8_weights)
     wbytes = st.info()["weight_bytes"]
-    st.set_engine(args.engine)
-    engine = st.engine(B)
     cs = torch.cuda.Stream()  # a real stream (the legacy default stream cannot be graph-captured)
     with torch.cuda.stream(cs):
         stream = cs.cuda_stream
@@ -164,11 +160,10 @@ def bench_single(args):
             past += 1
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        # roofline pass: the same decode steps, HIP events around the dominant kernel: the whole
-        # persistent step (class 4) or, on the launch engine, every weight GEMV (class 1, eager)
+        # roofline pass: the same decode steps, HIP events around every weight GEMV (class 1, eager)
         g_ms = g_n = g_bytes = 0
         if prof_steps:
-            st.profile_enable(4 if engine == "persistent" else 1)
+            st.profile_enable(1)
             for _ in range(prof_steps):
                 # the eager step's ~100 launches are enqueued behind a spin, so the event pairs time
                 # the GPU's execution, not the host's launch cadence
@@ -194,20 +189,15 @@ def bench_single(args):
                                "(BASELINE.json configs[1])",
                    "model": m.name, "stages": 1, "layers_per_stage": [m.n_layer], "batch": B, "prompt": P,
                    "ctx_range": [P + W, P + W + K], "parallelism": "pp1", "weight_bytes": wbytes,
-                   "engine": engine, "weights": args.weights},
+                   "weights": args.weights},
     }
     if g_n:
         avg_ms = g_ms / g_n
         ach = (g_bytes / g_n) / (avg_ms * 1e-3) / 1e9
-        if engine == "persistent":
-            tag, kname = "decode_engine", ("decode_engine_kernel: the whole decode step in one launch (all layers' "
-                                           "LN/QKV/attention/dense/fc1/fc2 + ln_f/lm_head/argmax)")
-            unit_note = "algorithmic bytes per launch = the step's weights + K/V read and append + hidden in/out"
-        else:
-            tag, kname = "gemv", "gemv_rows_kernel (every decode weight GEMV: LN+QKV, dense, LN+fc1, fc2, ln_f+lm_head)"
-            if args.weights == "int8":
-                kname = "gemv_q8_kernel (qkv, dense, fc1, fc2 on int8 weights) + gemv_rows_kernel (ln_f+lm_head, bf16)"
-            unit_note = "algorithmic bytes per launch = weights + bias + activations of the GEMV"
+        tag, kname = "gemv", "gemv_rows_kernel (every decode weight GEMV: LN+QKV, dense, LN+fc1, fc2, ln_f+lm_head)"
+        if args.weights == "int8":
+            kname = "gemv_q8_kernel (qkv, dense, fc1, fc2 on int8 weights) + gemv_rows_kernel (ln_f+lm_head, bf16)"
+        unit_note = "algorithmic bytes per launch = weights + bias + activations of the GEMV"
         traffic, note = (None, "--no-pmc") if args.no_pmc else pmc_traffic(args, tag)
         res["roofline"] = {"bound": "hbm", "kernel": kname,
                            "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,

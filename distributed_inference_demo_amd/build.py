@@ -3,6 +3,7 @@
     python -m distributed_inference_demo_amd.build          # incremental
     python -m distributed_inference_demo_amd.build --force
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -16,8 +17,9 @@ LIB = os.path.join(PKG, "lib", "libbloomstage.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "decode_engine.hip", "stage.hip", "codec.cpp"]
-HEADERS = ["common.h", "kernels.h", "decode_engine.h", "attn_merge.h"]
+SOURCES = ["kernels.hip", "stage.hip", "codec.cpp"]
+HEADERS = ["common.h", "kernels.h", "attn_merge.h"]
+STAMP = os.path.join(OBJ, "build_id")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-Wno-unused-result", "-Wno-unused-value", f"-I{os.path.join(ROOT, 'include')}"]
 
@@ -26,9 +28,22 @@ def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else 0.0
 
 
+def source_hash() -> str:
+    """SHA-256 over the library's sources (name + bytes, fixed order): the build provenance stamp
+    compiled into bs_build_id() and checked by stage.lib()."""
+    h = hashlib.sha256()
+    for path in [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "bloomstage.h")]:
+        with open(path, "rb") as f:
+            h.update(os.path.basename(path).encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    bid = source_hash()
+    old = open(STAMP).read().strip() if os.path.exists(STAMP) else ""
+    force = force or old != bid
     hdr_t = max([_mtime(os.path.join(CSRC, h)) for h in HEADERS] + [_mtime(os.path.join(ROOT, "include", "bloomstage.h"))])
     jobs = []
     objs = []
@@ -40,6 +55,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
             flags = list(CFLAGS)
             if src.endswith(".cpp"):
                 flags = [f for f in flags if not f.startswith("--offload-arch")] + ["-x", "c++"]
+            if src == "stage.hip":
+                flags.append(f'-DBS_BUILD_ID="{bid}"')
             jobs.append([HIPCC] + flags + ["-c", sp, "-o", op])
 
     def run(cmd):
@@ -56,6 +73,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
                 print(err)
     if jobs or not os.path.exists(LIB) or any(_mtime(o) > _mtime(LIB) for o in objs):
         run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs)
+    with open(STAMP, "w") as f:
+        f.write(bid)
     return LIB
 
 

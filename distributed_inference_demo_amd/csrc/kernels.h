@@ -24,12 +24,14 @@ struct Epi {
   void* v_cache;
   int hidden, head_dim, max_ctx, n_head;
   int seq, slot;
-  const int* past_dev;    // device scalar past_len (graph-replayable); used when non-null
-  int past;               // host past_len otherwise
+  const int* past_dev;    // device past_len per row b = m / seq (graph-replayable); used when non-null
+  int past;               // host past_len of every row otherwise
   // EPI_ARGMAX
   unsigned long long* keys;  // [M][N/16]: max over each 16-column tile
   float* logits;          // optional [M][ldo]
   int col_offset;         // vocabulary index of column 0 (head slices)
+  int key_hi_index;       // 0: keys rank equal logits by the LOWER index (greedy, torch.argmax);
+                          // 1: by the HIGHER index (top-k sampling, decoding.cpp:44-45 std::greater)
   // split-K workspace of the batched GEMV (gemv_tiles): fp32 partials [ks][M][N] (capacity in
   // floats) and one arrival ticket per 16-column tile (zero between launches).  Null: no split-K.
   float* sk_ws;
@@ -70,7 +72,7 @@ struct AttnArgs {
   void* ctx_out;       // T [B*S][hidden]
   const float* slopes; // [n_head]
   int B, S, slot;
-  const int* past_dev; // device past_len (graph-replayable) or null
+  const int* past_dev; // device past_len per row [B] (graph-replayable) or null
   int past;
   int n_head, head_dim, max_ctx, hidden;
   float inv_norm;
@@ -101,7 +103,14 @@ void launch_linear_parts(const AttnParts& p, const void* W, int M, int N, int K,
 // Reduce the per-tile keys of each row (and keys_in[m] if given) -> keys_out[m] / tokens[m] (either optional).
 void launch_argmax_finalize(const unsigned long long* keys, int M, int ntiles, const unsigned long long* keys_in,
                             unsigned long long* keys_out, int* tokens, hipStream_t s);
-void launch_set_past(int* past_dev, int value, hipStream_t s);
+// past_dev[0..n) = values[0..n) (host), stream ordered, by kernel arguments (graph-capturable).
+// Seeded top-k sampling (include/bloomstage.h bs_set_sampling; decoding.cpp:24-66) of M rows from the
+// per-16-column tile keys (key_hi_index = 1) and the logits they came from ([M][ldl], column = vocab index).
+// Row b's draw is keyed by (seed, KV row slot + b, position past_dev[b] + seq).
+void launch_topk_sample(const unsigned long long* keys, int ntiles, const float* logits, int ldl, int M, int k,
+                        float inv_temp, uint64_t seed, int slot, const int* past_dev, int seq, int* tokens,
+                        hipStream_t s);
+void launch_set_past(int* past_dev, const int* values, int n, hipStream_t s);
 
 // ---- Weight-only int8 (bf16 stages with BS_FLAG_INT8_WEIGHTS; kernels.hip "Weight-only int8") ----
 // Q[n][k] = rne(W[n][k] / scale[n]), scale[n] = max_k |W[n][k]| / 127 (1 for a zero row); W bf16 [N][K].

@@ -151,8 +151,9 @@ void launch_layernorm(int is_bf16, const void* x, const int* ids, int row_stride
 // 16 consecutive lanes (same lane>>4) hold the 16 columns of one output row: reduce the
 // (value, column) argmax over them and let the column-0 lane store the tile's key.
 __device__ __forceinline__ void argmax_tile16(const Epi& e, int m, int n, float v, bool valid, int ntiles) {
+  const uint32_t col = (uint32_t)(n + e.col_offset);
   unsigned long long key =
-      valid ? (((unsigned long long)f32_order_key(v) << 32) | (0xFFFFFFFFu - (uint32_t)(n + e.col_offset))) : 0ull;
+      valid ? (((unsigned long long)f32_order_key(v) << 32) | (e.key_hi_index ? col : 0xFFFFFFFFu - col)) : 0ull;
 #pragma unroll
   for (int o = 8; o >= 1; o >>= 1) {
     unsigned long long other = __shfl_xor(key, o, 64);
@@ -173,7 +174,7 @@ __device__ __forceinline__ void epi_store(const Epi& e, int m, int n, float v) {
       ((T*)e.q_out)[(size_t)m * e.hidden + head * e.head_dim + d] = from_f32<T>(v);
     } else {
       const int b = m / e.seq, t = m - b * e.seq;
-      const int past = e.past_dev ? *e.past_dev : e.past;
+      const int past = e.past_dev ? e.past_dev[b] : e.past;
       const size_t idx = (((size_t)(e.slot + b) * e.n_head + head) * e.max_ctx + past + t) * e.head_dim + d;
       T* c = (T*)(which == 1 ? e.k_cache : e.v_cache);
       c[idx] = from_f32<T>(v);
@@ -200,7 +201,7 @@ __device__ __forceinline__ EpiPre epi_prefetch(const Epi& e, int m, int n, bool 
   if (!valid || e.kind == EPI_ARGMAX) return p;
   p.bias = to_f32(((const T*)e.bias)[n]);
   if (e.kind == EPI_RESID) p.resid = e.resid[(size_t)m * e.ldo + n];
-  if (e.kind == EPI_QKV) p.past = e.past_dev ? *e.past_dev : e.past;
+  if (e.kind == EPI_QKV) p.past = e.past_dev ? e.past_dev[m / e.seq] : e.past;
   return p;
 }
 
@@ -1403,7 +1404,7 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   // q, the slope and past_len are independent of each other: all in flight with the first chunk
   const float slope = a.slopes[head];
   const float qreg = threadIdx.x < hd ? to_f32(((const T*)a.q)[(size_t)b * a.hidden + head * hd + threadIdx.x]) : 0.f;
-  const int past = a.past_dev ? *a.past_dev : a.past;
+  const int past = a.past_dev ? a.past_dev[b] : a.past;
   const int nk = past + 1, nlast = nk - 1;
   const int nch = (nk + CH - 1) / CH;
   if (threadIdx.x < hd) qs[threadIdx.x] = qreg;  // hd <= 128 <= WV * 64
@@ -1556,7 +1557,7 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(AttnArgs a) {
   __shared__ float qs[128];
   const int t = blockIdx.x, head = blockIdx.y, b = blockIdx.z, lane = threadIdx.x;
   const int hd = a.head_dim;
-  const int past = a.past_dev ? *a.past_dev : a.past;
+  const int past = a.past_dev ? a.past_dev[b] : a.past;
   const int nk = past + t + 1;
   const int m = b * a.S + t;
   for (int d = lane; d < hd; d += 64) qs[d] = to_f32(((const T*)a.q)[(size_t)m * a.hidden + head * hd + d]);
@@ -1607,10 +1608,12 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(AttnArgs a) {
 // mask + online softmax on the accumulator layout (row = 4*(lane>>4)+i, key = lane&15; row
 // reductions by DPP inside the 16-lane row); P -> fp16 through LDS into the A operand of the P.V
 // MFMAs (v_mfma_f32_16x16x32_f16; V is staged as fp16 — exact for bf16 values in fp16's normal
-// range — so P keeps 10 mantissa bits instead of 7).  q is bf16 (the stage stores q in the
+// range).  P is split into fp16(p) + fp16(p - fp16(p)) and both halves run through the P.V MFMAs,
+// so P keeps ~21 bits like the fp32 P of the checker (one fp16 P alone moved bloom-1b1's 512-token
+// prefill logits 2.06e-2 off the bf16-mode checker).  q is bf16 (the stage stores q in the
 // activation dtype); accumulation and softmax fp32.  The heaviest query tiles (most keys under
 // the causal mask) are dispatched first.
-template <int HDP>  // head_dim padded to a multiple of 32 (64, 96, 128)
+template <int HDP, bool PLO = true>  // head_dim padded to a multiple of 32 (64, 96, 128); PLO: P hi + lo
 __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   constexpr int KT = 64;                 // keys per tile
   constexpr int KS = HDP / 32;           // k-steps of S = Q.K^T
@@ -1621,10 +1624,11 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 Ks[KT * KLD];
   __shared__ __attribute__((aligned(16))) _Float16 Vt[HDP * VLD];
   __shared__ __attribute__((aligned(16))) _Float16 Ps[4][16 * VLD];
+  __shared__ __attribute__((aligned(16))) _Float16 Pl[4][16 * VLD];  // p - fp16(p): P keeps ~21 bits
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
   const int qt = gridDim.x - 1 - blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int hd = a.head_dim;
-  const int past = a.past_dev ? *a.past_dev : a.past;
+  const int past = a.past_dev ? a.past_dev[b] : a.past;
   const int q0 = qt * 64 + w * 16;          // first query (within this call) of the wave
   const bf16* qg = (const bf16*)a.q;
   // Q fragments: lane holds Q[q0 + r][ks*32 + 8g .. +8]
@@ -1760,17 +1764,27 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < 4; t++)
 #pragma unroll
-      for (int i = 0; i < 4; i++) Ps[w][(4 * g + i) * VLD + t * 16 + r] = (_Float16)sv[t][i];
+      for (int i = 0; i < 4; i++) {
+        const _Float16 hi = (_Float16)sv[t][i];
+        Ps[w][(4 * g + i) * VLD + t * 16 + r] = hi;
+        Pl[w][(4 * g + i) * VLD + t * 16 + r] = (_Float16)(sv[t][i] - (float)hi);
+      }
     __builtin_amdgcn_wave_barrier();
     typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
     const f16x8 pf0 = *reinterpret_cast<const f16x8*>(&Ps[w][r * VLD + 8 * g]);
     const f16x8 pf1 = *reinterpret_cast<const f16x8*>(&Ps[w][r * VLD + 32 + 8 * g]);
+    const f16x8 pl0 = *reinterpret_cast<const f16x8*>(&Pl[w][r * VLD + 8 * g]);
+    const f16x8 pl1 = *reinterpret_cast<const f16x8*>(&Pl[w][r * VLD + 32 + 8 * g]);
 #pragma unroll
     for (int t = 0; t < NT; t++) {
       const f16x8 vf0 = *reinterpret_cast<const f16x8*>(&Vt[vsw(t * 16 + r, 8 * g)]);
       const f16x8 vf1 = *reinterpret_cast<const f16x8*>(&Vt[vsw(t * 16 + r, 32 + 8 * g)]);
       o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf0, vf0, o[t], 0, 0, 0);
       o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf1, vf1, o[t], 0, 0, 0);
+      if constexpr (PLO) {
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl0, vf0, o[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl1, vf1, o[t], 0, 0, 0);
+      }
     }
   }
   // write ctx rows (q = q0 + 4g + i, dim = t*16 + r)
@@ -1837,7 +1851,12 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
     if (is_bf16 && a.head_dim <= 128) {
       dim3 g((a.S + 63) / 64, a.n_head, a.B);
       const int hdp = (a.head_dim + 31) / 32 * 32;
-      if (hdp <= 64) attn_prefill_mfma_kernel<64><<<g, 256, 0, s>>>(a);
+      static const bool plo = [] { const char* e = getenv("BS_ATTN_PLO"); return !(e && *e == '0'); }();  // A/B
+      if (!plo) {
+        if (hdp <= 64) attn_prefill_mfma_kernel<64, false><<<g, 256, 0, s>>>(a);
+        else if (hdp <= 96) attn_prefill_mfma_kernel<96, false><<<g, 256, 0, s>>>(a);
+        else attn_prefill_mfma_kernel<128, false><<<g, 256, 0, s>>>(a);
+      } else if (hdp <= 64) attn_prefill_mfma_kernel<64><<<g, 256, 0, s>>>(a);
       else if (hdp <= 96) attn_prefill_mfma_kernel<96><<<g, 256, 0, s>>>(a);
       else attn_prefill_mfma_kernel<128><<<g, 256, 0, s>>>(a);
     } else {
@@ -1888,8 +1907,134 @@ void launch_argmax_finalize(const unsigned long long* keys, int M, int ntiles, c
   argmax_finalize_kernel<<<M, 1024, 0, s>>>(keys, ntiles, keys_in, keys_out, tokens);
 }
 
-__global__ void set_past_kernel(int* p, int v) { *p = v; }
-void launch_set_past(int* past_dev, int value, hipStream_t s) { set_past_kernel<<<1, 1, 0, s>>>(past_dev, value); }
+// ------------------------------------------------------------------------------------
+// Seeded top-k sampling, restating decoding::StaticDecoding (decoding.cpp:24-66) on the tile keys of
+// the lm_head epilogue (key = order(logit) << 32 | vocab index: std::greater on (value, index)).
+// One 1024-thread block per row.  (1) The top-k TILES by their max key: every element of the row's
+// top-k lies in one of them (a tile outside holds an element below k tile maxima, i.e. below k
+// elements).  (2) The top-k elements among those k x 16 logits.  (3) w_i = exp((l_i - l_0) / T),
+// running sums in rank order, pick the first i with sum_{j<=i} w_j > u * sum(w) (u from the counter
+// generator), else the last.  k rounds of a block-wide max, each removing the winner, do the
+// selections; keys are unique (the index is in the key).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long other = __shfl_xor(v, o, 64);
+    v = other > v ? other : v;
+  }
+  return v;
+}
+
+// Block-wide max over 1024 threads (sh: >= 17 words); every thread returns the max.
+__device__ __forceinline__ unsigned long long block_max_u64(unsigned long long v, unsigned long long* sh) {
+  v = wave_max_u64(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    unsigned long long t = threadIdx.x < (blockDim.x >> 6) ? sh[threadIdx.x] : 0ull;
+    t = wave_max_u64(t);
+    if (threadIdx.x == 0) sh[16] = t;
+  }
+  __syncthreads();
+  const unsigned long long r = sh[16];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ uint32_t sample_bits(uint64_t seed, uint32_t row, uint32_t pos) {
+  const uint64_t key = d_sm64(seed ^ d_sm64(0x5A4D504C00000000ull | (uint64_t)row));
+  return d_bits(key, pos);
+}
+
+__global__ __launch_bounds__(1024) void topk_sample_kernel(const unsigned long long* __restrict__ keys, int ntiles,
+                                                           const float* __restrict__ logits, int ldl, int k,
+                                                           float inv_temp, uint64_t seed, int slot,
+                                                           const int* __restrict__ past_dev, int seq,
+                                                           int* __restrict__ tokens) {
+  __shared__ unsigned long long sh[17];
+  __shared__ unsigned long long pick[16];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  // (1) per-thread sorted top-16 of its tile keys, then k rounds of the block max
+  unsigned long long loc[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) loc[j] = 0ull;
+  const unsigned long long* kr = keys + (size_t)b * ntiles;
+  for (int i = tid; i < ntiles; i += 1024) {
+    unsigned long long key = kr[i];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const unsigned long long hi = key > loc[j] ? key : loc[j], lo = key > loc[j] ? loc[j] : key;
+      loc[j] = hi;
+      key = lo;
+    }
+  }
+  for (int r = 0; r < k; r++) {
+    const unsigned long long m = block_max_u64(loc[0], sh);
+    if (tid == 0) pick[r] = m;
+    if (loc[0] == m) {  // the unique owner drops its head
+#pragma unroll
+      for (int j = 0; j < 15; j++) loc[j] = loc[j + 1];
+      loc[15] = 0ull;
+    }
+  }
+  __syncthreads();
+  // (2) the k x 16 candidate logits of those tiles, ranked by (value, index)
+  unsigned long long cand = 0ull;
+  if (tid < k * 16 && pick[tid >> 4] != 0ull) {
+    const uint32_t col = ((uint32_t)(pick[tid >> 4] & 0xFFFFFFFFull) & ~15u) + (tid & 15);
+    if ((int)col < ldl) cand = ((unsigned long long)f32_order_key(logits[(size_t)b * ldl + col]) << 32) | col;
+  }
+  __shared__ float pv[16];
+  __shared__ int pi[16];
+  for (int r = 0; r < k; r++) {
+    const unsigned long long m = block_max_u64(cand, sh);
+    if (cand == m && m != 0ull) {
+      pv[r] = logits[(size_t)b * ldl + (uint32_t)(m & 0xFFFFFFFFull)];
+      pi[r] = (int)(uint32_t)(m & 0xFFFFFFFFull);
+      cand = 0ull;
+    }
+  }
+  __syncthreads();
+  // (3) weights, running sum, the draw
+  if (tid == 0) {
+    float w[16], sum = 0.f;
+    for (int r = 0; r < k; r++) {
+      w[r] = expf((pv[r] - pv[0]) * inv_temp);
+      sum += w[r];
+    }
+    const int pos = past_dev[b] + seq;
+    const float u = (float)(sample_bits(seed, (uint32_t)(slot + b), (uint32_t)pos) >> 8) * 0x1p-24f;
+    const float target = u * sum;
+    float run = 0.f;
+    int sel = k - 1;
+    for (int r = 0; r < k; r++) {
+      run += w[r];
+      if (run > target) { sel = r; break; }
+    }
+    tokens[b] = pi[sel];
+  }
+}
+
+void launch_topk_sample(const unsigned long long* keys, int ntiles, const float* logits, int ldl, int M, int k,
+                        float inv_temp, uint64_t seed, int slot, const int* past_dev, int seq, int* tokens,
+                        hipStream_t s) {
+  if (M > 0) topk_sample_kernel<<<M, 1024, 0, s>>>(keys, ntiles, logits, ldl, k, inv_temp, seed, slot, past_dev, seq, tokens);
+}
+
+// Per-row cached positions, passed by value (graph-replayable: the kernels read the device copy).
+struct PastRows { int v[64]; };
+__global__ void set_past_kernel(int* p, PastRows r, int n) {
+  if ((int)threadIdx.x < n) p[threadIdx.x] = r.v[threadIdx.x];
+}
+void launch_set_past(int* past_dev, const int* values, int n, hipStream_t s) {
+  for (int i = 0; i < n; i += 64) {
+    PastRows r;
+    const int c = std::min(64, n - i);
+    for (int j = 0; j < c; j++) r.v[j] = values[i + j];
+    set_past_kernel<<<1, 64, 0, s>>>(past_dev + i, r, c);
+  }
+}
 
 // ------------------------------------------------------------------------------------
 // Weight-only int8 (BS_FLAG_INT8_WEIGHTS): the four block matrices of a bf16 stage held as int8

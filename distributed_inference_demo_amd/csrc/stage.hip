@@ -17,7 +17,6 @@
 
 #include "../../include/bloomstage.h"
 #include "kernels.h"
-#include "decode_engine.h"
 
 static thread_local std::string g_err;
 
@@ -120,24 +119,13 @@ struct bs_stage {
   std::vector<std::pair<void*, size_t>> order;  // canonical weight order (BS_WEIGHTS_HOST layout)
   std::vector<std::pair<const float*, int>> order_q8;  // per order entry: (row scales, K) if int8, else (null, 0)
   std::vector<std::pair<GraphKey, hipGraphExec_t>> graphs;  // captured decode steps
-  // persistent decode engine (decode_engine.hip): one launch per decode step, B <= 4
-  int engine_mode = 0;          // bs_set_engine: 0 auto, 1 launches only, 2 persistent required
-  int de_grid[3] = {0, 0, 0};   // workgroups for MM = 1, 2, 4 (0 = unavailable)
-  size_t de_lds[3] = {0, 0, 0};
-  int de_maxrows = 0;
-  DeLayer* de_layers = nullptr;
-  char* de_state = nullptr;     // counters | tickets | fin | err
-  size_t de_state_bytes = 0;
-  unsigned *de_ctr = nullptr, *de_tick = nullptr, *de_fin = nullptr, *de_err = nullptr;
-  int de_ctr_words = 0, de_tick_words = 0;
-  unsigned* de_err_log = nullptr;   // sticky give-up codes (not touched by the kernel's re-zeroing)
-  char* de_ws = nullptr;            // x0 | xb0 | xb1 | part | wgkeys
-  float *de_x0 = nullptr, *de_xb0 = nullptr, *de_xb1 = nullptr, *de_part = nullptr;
-  unsigned long long* de_wgkeys = nullptr;
-  unsigned long long* de_trace = nullptr;  // BS_ENGINE_TRACE=1: phase stamps of the last launch
-  int de_trace_stride = 0;
   float* logit_buf = nullptr;       // host-I/O logits staging
   size_t logit_cap = 0;
+  // tail token pick (bs_set_sampling): top_k <= 1 greedy, else seeded top-k sampling
+  int top_k = 1;
+  float temperature = 1.f;
+  uint64_t sample_seed = 0;
+  float* sample_logits = nullptr;   // [max_batch][V] logits the sampler reads (device I/O without logits)
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -217,6 +205,11 @@ extern "C" uint64_t bs_stage_weight_count(const bs_stage_desc* d) {
 
 extern "C" int bs_abi_version(void) { return BS_ABI_VERSION; }
 
+#ifndef BS_BUILD_ID
+#define BS_BUILD_ID "unstamped"
+#endif
+extern "C" const char* bs_build_id(void) { return BS_BUILD_ID; }
+
 static uint32_t host_lb32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
@@ -240,148 +233,11 @@ static void free_stage(bs_stage* s) {
   if (s->wbase) hipFree(s->wbase);
   if (s->kv) hipFree(s->kv);
   if (s->ws) hipFree(s->ws);
-  if (s->de_layers) hipFree(s->de_layers);
-  if (s->de_state) hipFree(s->de_state);
-  if (s->de_ws) hipFree(s->de_ws);
   if (s->logit_buf) hipFree(s->logit_buf);
+  if (s->sample_logits) hipFree(s->sample_logits);
   if (s->wtmp) hipFree(s->wtmp);
-  if (s->de_trace) hipFree(s->de_trace);
   if (s->own) hipStreamDestroy(s->own);
   delete s;
-}
-
-// ---- persistent decode engine: eligibility, state and per-stage tables (decode_engine.h)
-static int engine_init(bs_stage* s) {
-  const bs_stage_desc& d = s->d;
-  const int h = d.hidden, nh = d.n_head;
-  if (!s->bf16 || s->q8 || h % 512 || h > 4096 || s->L < 1) return BS_OK;   // not eligible: launches only
-  if (s->kv_half * 2 >= (size_t)0xFFFFFFFFu) return BS_OK;        // 32-bit buffer offsets into one layer's KV
-  int cus = 0;
-  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d.device));
-  auto ceil_div = [](long a, long b) { return (int)((a + b - 1) / b); };
-  int maxrows = std::max(ceil_div(3L * h, cus), ceil_div(4L * h, cus));
-  if (d.is_last) maxrows = std::max(maxrows, ceil_div((long)d.vocab, cus));
-  s->de_maxrows = maxrows;
-  const int mms[3] = {1, 2, 4};
-  for (int i = 0; i < 3; i++) {
-    s->de_lds[i] = engine_lds_bytes(mms[i], h, maxrows);
-    s->de_grid[i] = engine_prepare(mms[i], s->de_lds[i], d.device);
-  }
-  if (!s->de_grid[0]) return BS_OK;
-  // sync state: edge counters, merge tickets, final ticket, error word
-  s->de_ctr_words = s->L * 5 * 8 * 16;
-  s->de_tick_words = s->L * 4 * nh;
-  const size_t ctr_b = (size_t)s->de_ctr_words * 4, tick_b = align_up((size_t)s->de_tick_words * 4, 256);
-  s->de_state_bytes = ctr_b + tick_b + 256 + 256 + 256;
-  if (hipMalloc(&s->de_state, s->de_state_bytes) != hipSuccess) return fail(BS_ERR_OOM, "engine state allocation failed");
-  s->de_ctr = (unsigned*)s->de_state;
-  s->de_tick = (unsigned*)(s->de_state + ctr_b);
-  s->de_fin = (unsigned*)(s->de_state + ctr_b + tick_b);
-  s->de_err = (unsigned*)(s->de_state + ctr_b + tick_b + 256);
-  s->de_err_log = (unsigned*)(s->de_state + ctr_b + tick_b + 512);
-  HIP_TRY(hipMemsetAsync(s->de_state, 0, s->de_state_bytes, s->own));
-  // workspace: x0, xb0, xb1 (fp32 [4][h]), attention partials, per-workgroup argmax keys
-  const size_t rowb = align_up((size_t)4 * h * 4, 256);
-  const size_t partb = align_up((size_t)std::max(4 * nh, cus) * (s->hd + 2) * 4, 256);
-  const size_t keyb = align_up((size_t)cus * 4 * 8, 256);
-  if (hipMalloc(&s->de_ws, 3 * rowb + partb + keyb) != hipSuccess) return fail(BS_ERR_OOM, "engine workspace allocation failed");
-  s->de_x0 = (float*)s->de_ws;
-  s->de_xb0 = (float*)(s->de_ws + rowb);
-  s->de_xb1 = (float*)(s->de_ws + 2 * rowb);
-  s->de_part = (float*)(s->de_ws + 3 * rowb);
-  s->de_wgkeys = (unsigned long long*)(s->de_ws + 3 * rowb + partb);
-  // per-layer pointer table
-  std::vector<DeLayer> tab(s->L);
-  for (int l = 0; l < s->L; l++) {
-    const Layer& w = s->layers[l];
-    DeLayer& t = tab[l];
-    t.ln1_g = (const bf16*)w.t[T_LN1_G]; t.ln1_b = (const bf16*)w.t[T_LN1_B];
-    t.wqkv = (const bf16*)w.t[T_QKV_W]; t.bqkv = (const bf16*)w.t[T_QKV_B];
-    t.wo = (const bf16*)w.t[T_DENSE_W]; t.bo = (const bf16*)w.t[T_DENSE_B];
-    t.ln2_g = (const bf16*)w.t[T_LN2_G]; t.ln2_b = (const bf16*)w.t[T_LN2_B];
-    t.w1 = (const bf16*)w.t[T_FC1_W]; t.b1 = (const bf16*)w.t[T_FC1_B];
-    t.w2 = (const bf16*)w.t[T_FC2_W]; t.b2 = (const bf16*)w.t[T_FC2_B];
-    t.kc = (bf16*)(s->kv + l * s->kv_layer_stride);
-    t.vc = (bf16*)(s->kv + l * s->kv_layer_stride + s->kv_half);
-  }
-  const char* tr = getenv("BS_ENGINE_TRACE");
-  if (tr && *tr && *tr != '0') {
-    s->de_trace_stride = 1 + 12 * s->L + 4;
-    if (hipMalloc(&s->de_trace, (size_t)cus * s->de_trace_stride * 8) != hipSuccess)
-      return fail(BS_ERR_OOM, "engine trace allocation failed");
-    HIP_TRY(hipMemsetAsync(s->de_trace, 0, (size_t)cus * s->de_trace_stride * 8, s->own));
-  }
-  if (hipMalloc(&s->de_layers, tab.size() * sizeof(DeLayer)) != hipSuccess) return fail(BS_ERR_OOM, "engine table");
-  HIP_TRY(hipMemcpyAsync(s->de_layers, tab.data(), tab.size() * sizeof(DeLayer), hipMemcpyHostToDevice, s->own));
-  HIP_TRY(hipStreamSynchronize(s->own));
-  return BS_OK;
-}
-
-static int engine_mm_index(int B) { return B <= 1 ? 0 : (B <= 2 ? 1 : 2); }
-
-// BS_ENGINE_AUTO resolves to the launch engine until the persistent one measures faster on the
-// bench workload (profiles/r01_engine_trace.log); BS_DECODE_ENGINE=persistent in the environment
-// flips the default for every stage.
-static int default_engine() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("BS_DECODE_ENGINE");
-    v = (e && !strcmp(e, "persistent")) ? 2 : 1;
-  }
-  return v;
-}
-
-static bool engine_eligible(const bs_stage* s, int B, int S) {
-  const int mode = s->engine_mode ? s->engine_mode : default_engine();
-  if (mode == 1 || S != 1 || B > 4 || B < 1) return false;
-  return s->de_grid[engine_mm_index(B)] > 0;
-}
-
-// Give-up codes of earlier engine launches (the launch that gave up already re-zeroed its counters;
-// its outputs are garbage).  Synchronizes `st`; clears the log.
-static int engine_take_errors(bs_stage* s, hipStream_t st, unsigned* code) {
-  *code = 0;
-  if (!s->de_err_log) return BS_OK;
-  HIP_TRY(hipStreamSynchronize(st));
-  HIP_TRY(hipMemcpy(code, s->de_err_log, 4, hipMemcpyDeviceToHost));
-  if (*code) HIP_TRY(hipMemset(s->de_err_log, 0, 4));
-  return BS_OK;
-}
-
-extern "C" int bs_engine_status(bs_stage* s, uint32_t* code) {
-  if (!s || !code) return fail(BS_ERR_INVALID, "stage/code is NULL");
-  HIP_TRY(hipSetDevice(s->d.device));
-  return engine_take_errors(s, s->own, code);
-}
-
-extern "C" int bs_engine_trace(bs_stage* s, uint64_t* out, uint64_t cap, int32_t* n_wg, int32_t* stride) {
-  if (!s || !n_wg || !stride) return fail(BS_ERR_INVALID, "stage/n_wg/stride is NULL");
-  if (!s->de_trace) return fail(BS_ERR_STATE, "engine trace not enabled (set BS_ENGINE_TRACE=1 before bs_init_stage)");
-  *n_wg = s->de_grid[0];
-  *stride = s->de_trace_stride;
-  const size_t n = (size_t)s->de_grid[0] * s->de_trace_stride;
-  if (out) {
-    if (cap < n) return fail(BS_ERR_INVALID, "trace buffer too small");
-    HIP_TRY(hipSetDevice(s->d.device));
-    HIP_TRY(hipStreamSynchronize(s->own));
-    HIP_TRY(hipMemcpy(out, s->de_trace, n * 8, hipMemcpyDeviceToHost));
-  }
-  return BS_OK;
-}
-
-extern "C" int bs_set_engine(bs_stage* s, int32_t mode) {
-  if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
-  if (mode < 0 || mode > 2) return fail(BS_ERR_INVALID, "engine mode must be 0 (auto), 1 (launches) or 2 (persistent)");
-  if (mode == 2 && !s->de_grid[0])
-    return fail(BS_ERR_UNSUPPORTED, "persistent decode engine unavailable for this stage (bf16, hidden % 512 == 0, "
-                                    "hidden <= 4096, >= 1 layer, resident on every CU)");
-  s->engine_mode = mode;
-  return BS_OK;
-}
-
-extern "C" int bs_get_engine(const bs_stage* s, int32_t batch) {
-  if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
-  return engine_eligible(s, batch, 1) ? 2 : 1;
 }
 
 extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
@@ -551,7 +407,7 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   wadd((size_t)desc->max_batch * (V / 16) * 8);
   wadd((size_t)desc->max_batch * 4);
   wadd(T * 4);
-  wadd(256);
+  wadd((size_t)desc->max_batch * 4);                 // per-row past_len (device copy)
   wadd((size_t)desc->max_batch * desc->n_head * 4);  // attention split-merge tickets
   wadd(kSkCap * 4);                                  // batched-GEMV split-K partials
   wadd(kSkTickets * 4);                              // and their tickets
@@ -583,8 +439,6 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   if (e != hipSuccess) return cleanup(fail(BS_ERR_DEVICE, std::string("init sync: ") + hipGetErrorString(e)));
   e = hipGetLastError();
   if (e != hipSuccess) return cleanup(fail(BS_ERR_DEVICE, std::string("init kernels: ") + hipGetErrorString(e)));
-  rc = engine_init(s);
-  if (rc != BS_OK) return cleanup(rc);
   *out = s;
   return BS_OK;
 }
@@ -729,18 +583,6 @@ static double gemv_bytes(const bs_stage* s, int M, int N, int K, int out_bytes) 
   return (double)N * K * s->esz + (double)N * s->esz + (double)M * K * s->esz + (double)M * N * out_bytes;
 }
 
-// Algorithmic HBM bytes of one engine decode step (BASELINE.md decode formula): every weight of
-// the stage once, each row's K/V cache read over past+1 positions and one row appended, the
-// first stage's embedding rows, the last stage's ln_f + lm_head, hidden in/out.
-static double engine_step_bytes(const bs_stage* s, int B, int past) {
-  const double h = s->d.hidden, w = (double)s->esz, k = (double)s->esz;
-  double b = s->L * ((12.0 * h * h + 13.0 * h) * w + 2.0 * B * (past + 1) * h * k);
-  if (s->d.is_first) b += B * h * w + 2.0 * h * w;
-  if (s->d.is_last) b += (double)s->d.vocab * h * w + 2.0 * h * w;
-  b += 2.0 * B * h * 4.0;
-  return b;
-}
-
 // The forward's GEMVs may split K through the stage's workspace (see kSkCap).
 static Epi with_splitk(const bs_stage* s, const Epi& ep) {
   Epi e = ep;
@@ -822,12 +664,14 @@ static int logits_staging(bs_stage* s, size_t bytes, hipStream_t st, float** out
   return BS_OK;
 }
 
-// Enqueue one forward on `st`.  With `past_dev` set, kernels read past_len from device memory
-// (graph-replayable); otherwise from the host value.
+// Enqueue one forward on `st`.  The kernels read each row's past_len from past_dev (device [B],
+// written ahead of the forward or of the graph replay); `pasts` is the host copy (profiling bytes).
 static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, void* out, float* logits, hipStream_t st,
-                           const int* past_dev) {
+                           const int* past_dev, const std::vector<int>& pasts) {
   const bs_stage_desc& d = s->d;
-  const int B = step->batch, S = step->seq, slot = step->slot, past = step->past_len;
+  const int B = step->batch, S = step->seq, slot = step->slot, past = pasts[0];
+  double ctx_sum = 0.0;
+  for (int b = 0; b < B; b++) ctx_sum += (double)pasts[b] + S;
   const int M = B * S;
   const bool want_logits = (step->flags & BS_STEP_LOGITS) != 0;
   const bool host_io = (step->flags & BS_STEP_HOST_IO) != 0;
@@ -871,7 +715,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     const int nsplit = S == 1 ? attention_decode_splits(B, nh, s->max_chunks) : 1;
     a.defer_merge = s->bf16 && !s->q8 && nsplit > 1 && linear_parts_supported(M, h, hd, nsplit);
     {
-      ProfScope p(s, st, 3, (double)B * nh * (double)(past + S) * hd * 2 * s->esz);
+      ProfScope p(s, st, 3, ctx_sum * nh * hd * 2 * s->esz);
       launch_attention(s->bf16, a, st);
     }
     // a = x + dense(ctx)
@@ -898,17 +742,25 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
 
   // ---- output
   if (d.is_last) {
-    // ln_f on each row's last position, tied lm_head, greedy pick
+    // ln_f on each row's last position, tied lm_head, token pick (greedy argmax or top-k sample)
+    const bool sample = s->top_k > 1;
     Epi e{};
     e.kind = EPI_ARGMAX; e.keys = s->keys; e.logits = want_logits && !host_io ? logits : nullptr; e.ldo = V;
+    e.key_hi_index = sample ? 1 : 0;  // sampling ranks equal logits by the higher index (decoding.cpp:44-45)
     float* dev_logits = nullptr;
     if (want_logits && host_io) {
       int rc = logits_staging(s, (size_t)B * V * 4, st, &dev_logits);
       if (rc != BS_OK) return rc;
       e.logits = dev_logits;
     }
+    if (sample && !e.logits) e.logits = s->sample_logits;
     linear_ln(s, st, cur, S, S - 1, s->lnf_g, s->lnf_b, s->wemb, B, V, h, with_splitk(s, e), 0);
-    launch_argmax_finalize(s->keys, B, V / 16, nullptr, nullptr, host_io ? s->tok : (int*)out, st);
+    int* tok_out = host_io ? s->tok : (int*)out;
+    if (sample)
+      launch_topk_sample(s->keys, V / 16, e.logits, V, B, s->top_k, 1.0f / s->temperature, s->sample_seed, slot,
+                         past_dev, S, tok_out, st);
+    else
+      launch_argmax_finalize(s->keys, B, V / 16, nullptr, nullptr, tok_out, st);
     if (host_io) {
       HIP_TRY(hipMemcpyAsync(out, s->tok, (size_t)B * 4, hipMemcpyDeviceToHost, st));
       if (dev_logits) HIP_TRY(hipMemcpyAsync(logits, dev_logits, (size_t)B * V * 4, hipMemcpyDeviceToHost, st));
@@ -917,75 +769,6 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     HIP_TRY(hipMemcpyAsync(out, cur, (size_t)M * h * 4, hipMemcpyDeviceToHost, st));
   } else if (s->L == 0) {
     HIP_TRY(hipMemcpyAsync(out, cur, (size_t)M * h * 4, hipMemcpyDeviceToDevice, st));
-  }
-  return BS_OK;
-}
-
-// One decode step (S = 1, B <= 4) as ONE persistent launch (decode_engine.hip).
-static int engine_enqueue(bs_stage* s, const bs_step* step, const void* in, void* out, float* logits, hipStream_t st) {
-  const bs_stage_desc& d = s->d;
-  const int B = step->batch;
-  const bool host_io = (step->flags & BS_STEP_HOST_IO) != 0;
-  const bool want_logits = (step->flags & BS_STEP_LOGITS) != 0;
-  const int h = d.hidden, V = d.vocab;
-  const int mi = engine_mm_index(B), mm = mi == 0 ? 1 : (mi == 1 ? 2 : 4);
-  DeArgs a{};
-  a.layers = s->de_layers;
-  a.L = s->L; a.M = B; a.h = h; a.nh = d.n_head; a.hd = s->hd; a.max_ctx = d.max_ctx;
-  a.slot = step->slot; a.past = step->past_len;
-  a.kv_half_bytes = (unsigned)s->kv_half;
-  a.eps = d.ln_eps; a.inv_norm = 1.0f / std::sqrt((float)s->hd); a.slopes = s->slopes;
-  if (d.is_first) {
-    const int* ids = (const int*)in;
-    if (host_io) {
-      HIP_TRY(hipMemcpyAsync(s->ids, ids, (size_t)B * 4, hipMemcpyHostToDevice, st));
-      ids = s->ids;
-    }
-    a.ids = ids; a.wemb = (const bf16*)s->wemb; a.emb_g = (const bf16*)s->emb_g; a.emb_b = (const bf16*)s->emb_b;
-  } else if (host_io) {
-    HIP_TRY(hipMemcpyAsync(s->xa, in, (size_t)B * h * 4, hipMemcpyHostToDevice, st));
-    a.x_in = s->xa;
-  } else {
-    a.x_in = (const float*)in;
-  }
-  if (!d.is_last && !host_io) a.x_out = (float*)out;
-  a.xb0 = s->de_xb0; a.xb1 = s->de_xb1; a.attn = s->attn; a.x0 = s->de_x0;
-  a.q = (bf16*)s->q; a.ctx = (bf16*)s->ctx; a.g = (bf16*)s->g; a.part = s->de_part;
-  float* dev_logits = nullptr;
-  if (d.is_last) {
-    a.has_head = 1;
-    a.lnf_g = (const bf16*)s->lnf_g; a.lnf_b = (const bf16*)s->lnf_b; a.whead = (const bf16*)s->wemb;
-    a.head_rows = V; a.col_offset = 0;
-    a.wgkeys = s->de_wgkeys;
-    a.tokens = host_io ? s->tok : (int*)out;
-    if (want_logits) {
-      if (host_io) {
-        int rc = logits_staging(s, (size_t)B * V * 4, st, &dev_logits);
-        if (rc != BS_OK) return rc;
-      }
-      a.logits = host_io ? dev_logits : logits;
-      a.ldl = V;
-    }
-  }
-  a.ctr = s->de_ctr; a.n_ctr_words = s->de_ctr_words; a.tick = s->de_tick; a.n_tick_words = s->de_tick_words;
-  a.fin = s->de_fin; a.err = s->de_err; a.err_log = s->de_err_log;
-  a.trace = s->de_trace; a.trace_stride = s->de_trace_stride;
-  const size_t xs_b = (size_t)mm * 4 * h * 2, res_b = (size_t)mm * s->de_maxrows * 4;
-  a.lds_res = (int)align_up(xs_b, 16);
-  a.lds_scr = (int)(align_up(xs_b, 16) + align_up(res_b, 16));
-  a.maxrows = s->de_maxrows;
-  {
-    ProfScope p(s, st, 4, engine_step_bytes(s, B, step->past_len));
-    engine_launch(a, mm, s->de_grid[mi], s->de_lds[mi], st);
-  }
-  if (host_io) {
-    if (d.is_last) {
-      HIP_TRY(hipMemcpyAsync(out, s->tok, (size_t)B * 4, hipMemcpyDeviceToHost, st));
-      if (dev_logits) HIP_TRY(hipMemcpyAsync(logits, dev_logits, (size_t)B * V * 4, hipMemcpyDeviceToHost, st));
-    } else {
-      const float* res = ((s->L - 1) & 1) ? s->de_xb1 : s->de_xb0;
-      HIP_TRY(hipMemcpyAsync(out, res, (size_t)B * h * 4, hipMemcpyDeviceToHost, st));
-    }
   }
   return BS_OK;
 }
@@ -1020,6 +803,27 @@ extern "C" int bs_head_slice(bs_stage* s, const void* xn, int32_t B, const uint6
   return BS_OK;
 }
 
+extern "C" int bs_set_sampling(bs_stage* s, int32_t top_k, float temperature, uint64_t seed) {
+  if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
+  if (top_k > 16) return fail(BS_ERR_UNSUPPORTED, "top_k must be <= 16");
+  if (top_k > 1 && !s->d.is_last) return fail(BS_ERR_UNSUPPORTED, "sampling needs the last stage (whole lm_head)");
+  if (top_k > 1 && !(temperature > 0.f)) return fail(BS_ERR_INVALID, "temperature must be positive");
+  HIP_TRY(hipSetDevice(s->d.device));
+  if (top_k > 1 && !s->sample_logits) {
+    HIP_TRY(hipStreamSynchronize(s->own));
+    if (hipMalloc((void**)&s->sample_logits, (size_t)s->d.max_batch * s->d.vocab * 4) != hipSuccess)
+      return fail(BS_ERR_OOM, "sampling logits allocation failed");
+  }
+  s->top_k = top_k < 1 ? 1 : top_k;
+  s->temperature = top_k > 1 ? temperature : 1.f;
+  s->sample_seed = seed;
+  // captured decode graphs hold the old pick as kernel arguments
+  HIP_TRY(hipDeviceSynchronize());
+  for (auto& g : s->graphs) hipGraphExecDestroy(g.second);
+  s->graphs.clear();
+  return BS_OK;
+}
+
 static bool graphs_enabled() {
   static int on = -1;
   if (on < 0) {
@@ -1032,11 +836,15 @@ static bool graphs_enabled() {
 extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void* out, float* logits, void* stream) {
   if (!s || !step) return fail(BS_ERR_INVALID, "stage/step is NULL");
   const bs_stage_desc& d = s->d;
-  const int B = step->batch, S = step->seq, slot = step->slot, past = step->past_len;
+  const int B = step->batch, S = step->seq, slot = step->slot;
   const int M = B * S;
   if (B <= 0 || S <= 0) return fail(BS_ERR_INVALID, "batch and seq must be positive");
   if (slot < 0 || slot + B > d.max_batch) return fail(BS_ERR_INVALID, "slot range outside max_batch");
-  if (past < 0 || past + S > d.max_ctx) return fail(BS_ERR_INVALID, "past_len + seq exceeds max_ctx");
+  std::vector<int> pasts(B);
+  for (int b = 0; b < B; b++) {
+    pasts[b] = step->past_lens ? step->past_lens[b] : step->past_len;
+    if (pasts[b] < 0 || pasts[b] + S > d.max_ctx) return fail(BS_ERR_INVALID, "past_len + seq exceeds max_ctx");
+  }
   if (M > d.max_tokens) return fail(BS_ERR_INVALID, "batch*seq exceeds max_tokens");
   if (!in || !out) return fail(BS_ERR_INVALID, "in/out is NULL");
   const bool want_logits = (step->flags & BS_STEP_LOGITS) != 0;
@@ -1053,22 +861,7 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
   // Decode steps on device buffers replay a captured hipGraph: the kernels read past_len from
   // device memory, set by one small kernel ahead of the replay.
   const bool graph = S == 1 && !host_io && s->prof.cls == 0 && graphs_enabled();
-  if (engine_eligible(s, B, S)) {
-    int rc = engine_enqueue(s, step, in, out, logits, st);
-    if (rc != BS_OK) return rc;
-    if (host_io) {  // synchronous anyway: report a give-up of this (or an earlier) launch
-      unsigned code = 0;
-      rc = engine_take_errors(s, st, &code);
-      if (rc != BS_OK) return rc;
-      if (code) {
-        char buf[128];
-        snprintf(buf, sizeof buf, "persistent decode engine gave up waiting (code 0x%x); outputs invalid", code);
-        return fail(BS_ERR_DEVICE, buf);
-      }
-    }
-  } else if (s->engine_mode == 2 && S == 1) {
-    return fail(BS_ERR_UNSUPPORTED, "persistent decode engine requested but this decode step is not eligible (B <= 4)");
-  } else if (graph) {
+  if (graph) {
     GraphKey key{B, slot, step->flags, in, out, logits, st};
     hipGraphExec_t exec = nullptr;
     for (auto& g : s->graphs)
@@ -1076,7 +869,7 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
     if (!exec) {
       hipGraph_t gr = nullptr;
       HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
-      int rc = enqueue_forward(s, step, in, out, logits, st, s->past_dev);
+      int rc = enqueue_forward(s, step, in, out, logits, st, s->past_dev, pasts);
       hipError_t ce = hipStreamEndCapture(st, &gr);
       if (rc != BS_OK) { if (gr) hipGraphDestroy(gr); return rc; }
       if (ce != hipSuccess) return fail(BS_ERR_DEVICE, std::string("graph capture: ") + hipGetErrorString(ce));
@@ -1089,10 +882,11 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
       }
       s->graphs.push_back({key, exec});
     }
-    launch_set_past(s->past_dev, past, st);
+    launch_set_past(s->past_dev, pasts.data(), B, st);
     HIP_TRY(hipGraphLaunch(exec, st));
   } else {
-    int rc = enqueue_forward(s, step, in, out, logits, st, nullptr);
+    launch_set_past(s->past_dev, pasts.data(), B, st);
+    int rc = enqueue_forward(s, step, in, out, logits, st, s->past_dev, pasts);
     if (rc != BS_OK) return rc;
   }
   hipError_t err = hipGetLastError();

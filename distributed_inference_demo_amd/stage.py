@@ -67,7 +67,8 @@ class StageDesc(ctypes.Structure):
 
 class Step(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int32), ("seq", ctypes.c_int32), ("slot", ctypes.c_int32),
-                ("past_len", ctypes.c_int32), ("flags", ctypes.c_int32)]
+                ("past_len", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("past_lens", ctypes.POINTER(ctypes.c_int32))]
 
 
 class TensorView(ctypes.Structure):
@@ -79,11 +80,9 @@ EXPORTS = [
     "bs_init_stage", "bs_forward", "bs_reset_kv", "bs_release", "bs_last_error", "bs_stage_info",
     "bs_stage_weight_count", "bs_abi_version", "bs_profile_enable", "bs_profile_read",
     "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
-    "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice", "bs_set_engine", "bs_get_engine",
-    "bs_engine_status", "bs_engine_trace", "bs_stream_delay",
+    "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice", "bs_stream_delay", "bs_set_sampling",
+    "bs_build_id",
 ]
-
-ENGINE_AUTO, ENGINE_LAUNCHES, ENGINE_PERSISTENT = 0, 1, 2
 
 _LIB = None
 
@@ -100,6 +99,11 @@ def lib():
             raise BloomStageError(f"{LIB_PATH} not built: run `python -m distributed_inference_demo_amd.build`")
         L = ctypes.CDLL(LIB_PATH)
         vp, i32 = ctypes.c_void_p, ctypes.c_int32
+        L.bs_build_id.restype = ctypes.c_char_p
+        want, got = source_build_id(), L.bs_build_id().decode()
+        if want is not None and got != want:
+            raise BloomStageError(f"{LIB_PATH} was built from other sources (stamp {got[:12]}, sources {want[:12]}): "
+                                  "rebuild with `python -m distributed_inference_demo_amd.build`")
         L.bs_init_stage.argtypes = [ctypes.POINTER(StageDesc), ctypes.POINTER(vp)]
         L.bs_forward.argtypes = [vp, ctypes.POINTER(Step), vp, vp, vp, vp]
         L.bs_reset_kv.argtypes = [vp, i32]
@@ -125,12 +129,19 @@ def lib():
         L.bs_read_weights.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, vp]
         L.bs_head_norm.argtypes = [vp, vp, i32, i32, vp, vp]
         L.bs_head_slice.argtypes = [vp, vp, i32, vp, vp, vp, vp]
-        L.bs_set_engine.argtypes = [vp, i32]
-        L.bs_get_engine.argtypes = [vp, i32]
-        L.bs_engine_status.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
-        L.bs_engine_trace.argtypes = [vp, vp, ctypes.c_uint64, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        L.bs_set_sampling.argtypes = [vp, i32, ctypes.c_float, ctypes.c_uint64]
         _LIB = L
     return _LIB
+
+
+def source_build_id():
+    """SHA-256 of the library sources beside this file (the stamp build.py compiles into
+    bs_build_id); None when the sources are not present (an installed library)."""
+    from .build import source_hash
+    try:
+        return source_hash()
+    except FileNotFoundError:
+        return None
 
 
 def _check(rc):
@@ -186,40 +197,37 @@ class Stage:
         self._weights_ref = None  # uploaded; host copy no longer needed
         self.past = [0] * max_batch  # host mirror of cached positions per KV row
 
+    def _step(self, batch, seq, slot, past_len, flags):
+        """Step struct; past_len is an int (every row) or a sequence of per-row positions.
+        Returns (step, per-row pasts)."""
+        if past_len is None:
+            past_len = self.past[slot:slot + batch] if 0 <= slot and slot + batch <= len(self.past) else 0
+        if np.ndim(past_len) == 0:
+            pasts = [int(past_len)] * batch
+            st = Step(batch, seq, slot, int(past_len), flags, None)
+        else:
+            pasts = [int(p) for p in past_len]
+            if len(pasts) != batch:
+                raise BloomStageError(f"{len(pasts)} past lengths for {batch} rows")
+            arr = (ctypes.c_int32 * batch)(*pasts)
+            st = Step(batch, seq, slot, pasts[0], flags, arr)
+            st._keep = arr
+        return st, pasts
+
     # ---- fast path (device pointers, stream ordered)
     def forward(self, inp, out, batch, seq, slot=0, past_len=None, logits=None, stream=None):
-        past = self.past[slot] if past_len is None else past_len
-        st = Step(batch, seq, slot, past, BS_STEP_LOGITS if logits is not None else 0)
+        """past_len: positions already cached, one int for every row or one per row (None: the
+        host mirror of each row's position)."""
+        st, pasts = self._step(batch, seq, slot, past_len, BS_STEP_LOGITS if logits is not None else 0)
         _check(lib().bs_forward(self._h, ctypes.byref(st), _ptr(inp), _ptr(out), _ptr(logits), stream))
-        for r in range(slot, slot + batch):
-            self.past[r] = past + seq
+        for i, r in enumerate(range(slot, slot + batch)):
+            self.past[r] = pasts[i] + seq
         return out
 
-    # ---- decode engine selection (bs_set_engine): "auto", "launches" or "persistent"
-    def set_engine(self, mode):
-        m = {"auto": ENGINE_AUTO, "launches": ENGINE_LAUNCHES, "persistent": ENGINE_PERSISTENT}.get(mode, mode)
-        _check(lib().bs_set_engine(self._h, int(m)))
-
-    def engine(self, batch=1):
-        """Engine a decode step of `batch` rows runs on: "persistent" or "launches"."""
-        rc = lib().bs_get_engine(self._h, batch)
-        if rc < 0:
-            _check(rc)
-        return "persistent" if rc == ENGINE_PERSISTENT else "launches"
-
-    def engine_trace(self):
-        """Phase stamps of the last persistent launch, uint64 [workgroups][stride] (BS_ENGINE_TRACE=1)."""
-        n, st = ctypes.c_int32(), ctypes.c_int32()
-        _check(lib().bs_engine_trace(self._h, None, 0, ctypes.byref(n), ctypes.byref(st)))
-        out = np.empty((n.value, st.value), np.uint64)
-        _check(lib().bs_engine_trace(self._h, out.ctypes.data, out.size, ctypes.byref(n), ctypes.byref(st)))
-        return out
-
-    def engine_status(self):
-        """Give-up codes of persistent launches since the last call (0 = all launches completed)."""
-        code = ctypes.c_uint32(0)
-        _check(lib().bs_engine_status(self._h, ctypes.byref(code)))
-        return code.value
+    def set_sampling(self, top_k=1, temperature=1.0, seed=0):
+        """Tail token pick (bs_set_sampling): greedy for top_k <= 1, else seeded top-k sampling in
+        decoding.cpp:24-66's order (last stage only)."""
+        _check(lib().bs_set_sampling(self._h, int(top_k), float(temperature), int(seed)))
 
     # ---- vocabulary-parallel head (device pointers, stream ordered)
     def head_norm(self, hidden, batch, seq, xn, stream=None):
@@ -238,13 +246,12 @@ class Stage:
             x = np.ascontiguousarray(x, dtype=np.float32).reshape(batch, seq, self.hidden)
         out = np.empty(batch, np.int32) if self.is_last else np.empty((batch, seq, self.hidden), np.float32)
         logits = np.empty((batch, self.vocab), np.float32) if want_logits else None
-        past = self.past[slot] if past_len is None else past_len
         flags = BS_STEP_HOST_IO | (BS_STEP_LOGITS if want_logits else 0)
-        st = Step(batch, seq, slot, past, flags)
+        st, pasts = self._step(batch, seq, slot, past_len, flags)
         _check(lib().bs_forward(self._h, ctypes.byref(st), x.ctypes.data, out.ctypes.data,
                                 logits.ctypes.data if logits is not None else None, None))
-        for r in range(slot, slot + batch):
-            self.past[r] = past + seq
+        for i, r in enumerate(range(slot, slot + batch)):
+            self.past[r] = pasts[i] + seq
         return (out, logits) if want_logits else out
 
     def reset(self, slot=-1):
@@ -406,16 +413,19 @@ def run_inference_worker_residual(stage: Stage, seq_bytes: bytes, residuals=(), 
 def run_inference_worker_residual_last_generation(stage: Stage, seq_bytes: bytes, residuals=(), k: int = 1,
                                                   initial_temp: float = 1.0, seed: int = 0) -> bytes:
     """runInferenceWorkerResidualLastGeneration (native-lib.cpp:1368-1443): tail stage, returns the
-    next token id as 4 little-endian bytes (utils::SerializeInt)."""
+    next token id as 4 little-endian bytes (utils::SerializeInt).  k <= 1: greedy argmax; k > 1:
+    the device top-k pick of decoding::StaticDecoding (decoding.cpp:24-66, bs_set_sampling), seeded
+    by `seed` and keyed by the row's position, so every step draws afresh.  Like the reference
+    (decoding.cpp:51-52), initial_temp is accepted and not applied."""
     tensors = deserialize_tensors(seq_bytes)
     x = tensors[0].astype(np.float32, copy=False)
     S = x.shape[-2]
-    if k <= 1:
-        tok = stage.forward_host(x, 1, S)
-        return serialize_int(int(tok[0]))
-    tok, logits = stage.forward_host(x, 1, S, want_logits=True)
-    from .sampling import top_k_sample
-    return serialize_int(top_k_sample(logits[0], k, initial_temp, seed))
+    pick = (max(1, int(k)), int(seed))
+    if getattr(stage, "_pick", (1, 0)) != pick:
+        stage.set_sampling(pick[0], 1.0, pick[1])
+        stage._pick = pick
+    tok = stage.forward_host(x, 1, S)
+    return serialize_int(int(tok[0]))
 
 
 def unpack_int_be(data: bytes) -> int:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define BS_ABI_VERSION 1
+#define BS_ABI_VERSION 2
 
 typedef enum {
   BS_OK = 0,
@@ -96,13 +96,17 @@ typedef struct bs_stage_desc {
 
 typedef struct bs_stage bs_stage;
 
-/* One forward call over B rows x S new tokens. */
+/* One forward call over B rows x S new tokens.  Every KV row (slot) keeps its own position:
+ * the reference keeps core_pool_size samples in flight, each at its own position
+ * (Communication.java:418-464, :621-651), so rows of one call may sit at different positions. */
 typedef struct bs_step {
   int32_t batch;     /* B rows */
   int32_t seq;       /* S new tokens per row */
   int32_t slot;      /* first KV-cache row used by these B rows */
-  int32_t past_len;  /* positions already cached in those rows (same for all rows) */
+  int32_t past_len;  /* positions already cached in every row (used when past_lens is NULL) */
   int32_t flags;     /* BS_STEP_* */
+  const int32_t *past_lens;  /* host [B]: positions already cached in row slot+b (per-row context
+                                lengths, SURVEY.md §8b ctx_lens); NULL = past_len for all rows */
 } bs_step;
 
 #define BS_STEP_HOST_IO 1  /* in/out/logits are host pointers (copied in/out, stream-synchronous) */
@@ -116,7 +120,9 @@ int bs_init_stage(const bs_stage_desc *desc, bs_stage **out);
  *  out: last stage  -> int32 token ids [B] (greedy argmax of each row's last position);
  *       otherwise fp32 hidden [B][S][hidden]
  *  logits: fp32 [B][vocab] when step->flags & BS_STEP_LOGITS (last stage only), else NULL.
- * Appends S positions to KV rows [slot, slot+B). Positions are past_len .. past_len+S-1. */
+ * Appends S positions to KV rows [slot, slot+B): row b's new positions are p_b .. p_b+S-1 with
+ * p_b = past_lens[b] (or past_len).  The last stage's token pick is greedy argmax unless
+ * bs_set_sampling selected top-k sampling. */
 int bs_forward(bs_stage *stage, const bs_step *step, const void *in, void *out, float *logits,
                void *stream);
 
@@ -132,28 +138,18 @@ int bs_head_norm(bs_stage *stage, const float *hidden, int32_t batch, int32_t se
 int bs_head_slice(bs_stage *stage, const void *xn, int32_t batch, const uint64_t *keys_in, uint64_t *keys_out,
                   int32_t *tokens, void *stream);
 
-/* ---- Decode engine (S = 1 steps of B <= 4 rows on bf16 stages with hidden % 512 == 0) ----
- * BS_ENGINE_PERSISTENT: the whole stage step is ONE kernel launch, a workgroup per CU walking
- *   every layer (weights of the next op requested before waiting on the current one; in-launch
- *   hand-offs).  BS_ENGINE_LAUNCHES: one kernel per op, captured in a
- *   hipGraph.  BS_ENGINE_AUTO (default) is the launch engine unless BS_DECODE_ENGINE=persistent is
- *   set in the environment; the persistent engine runs only on eligible steps.
- * No reference counterpart: the reference has one engine (ORT Session::Run, inference.cpp:207-215). */
-#define BS_ENGINE_AUTO 0
-#define BS_ENGINE_LAUNCHES 1
-#define BS_ENGINE_PERSISTENT 2
-int bs_set_engine(bs_stage *stage, int32_t mode);
-/* Engine a decode step of `batch` rows would run on (BS_ENGINE_LAUNCHES or BS_ENGINE_PERSISTENT). */
-int bs_get_engine(const bs_stage *stage, int32_t batch);
-/* Give-up codes of persistent launches since the last call (0 = none).  A launch whose in-launch
- * wait exceeded 200 ms aborts: its outputs are invalid, the next launch starts clean.  Host-I/O
- * steps report this themselves as BS_ERR_DEVICE.  Synchronizes the stage's own stream. */
-int bs_engine_status(bs_stage *stage, uint32_t *code);
-/* Diagnostics: with BS_ENGINE_TRACE=1 in the environment at bs_init_stage, every persistent launch
- * stores one 100 MHz s_memrealtime stamp per workgroup at each phase boundary; this copies the last
- * launch's stamps ([n_wg][stride] uint64; index 0 = start, 1 + 12*layer + k, then the head).
- * out = NULL: only report n_wg and stride.  Synchronizes the stage's own stream. */
-int bs_engine_trace(bs_stage *stage, uint64_t *out, uint64_t cap, int32_t *n_wg, int32_t *stride);
+/* ---- Tail token pick (last stage) ----
+ * top_k <= 1: greedy argmax (the default; lowest index on ties, like torch.argmax).
+ * 2 <= top_k <= 16: seeded top-k sampling restating decoding::StaticDecoding (decoding.cpp:24-66):
+ *   the top_k (logit, index) pairs of each row's last position in std::greater order (larger logit
+ *   first, the HIGHER index first on equal logits: decoding.cpp:44-45), weights
+ *   w_i = exp((l_i - l_0) / temperature) -- with temperature 1 exactly the reference's "normalise
+ *   the top-k probabilities by their sum" (:56-57) applied to softmax probabilities -- and the pick
+ *   = the first i whose running sum of w exceeds u * sum(w), u in [0, 1) from the stage's counter
+ *   generator keyed by (seed, KV row, position): reproducible, unlike the reference's
+ *   std::random_device seed (:61-63).  The reference never applies its temperature argument
+ *   (:51-52); pass 1 to reproduce it.  Not available on vocabulary-slice (bs_head_slice) stages. */
+int bs_set_sampling(bs_stage *stage, int32_t top_k, float temperature, uint64_t seed);
 
 /* Forget the cached positions of one KV row (slot), or of all rows when slot < 0. */
 int bs_reset_kv(bs_stage *stage, int32_t slot);
@@ -171,6 +167,9 @@ int bs_stage_info(const bs_stage *stage, bs_stage_desc *out_desc, uint64_t *weig
  * [ln_f g,b if a slice is set and the stage is not last]. */
 uint64_t bs_stage_weight_count(const bs_stage_desc *desc);
 int bs_abi_version(void);
+/* Build provenance: hex SHA-256 of the library's sources (csrc files and include/bloomstage.h) stamped at
+ * compile time; the Python binding refuses a library whose stamp differs from the sources beside it. */
+const char *bs_build_id(void);
 /* Read back `count` weights starting at element `offset` of the canonical stage order
  * (the BS_WEIGHTS_HOST layout) as fp32.  For verification of loaded/generated weights. */
 int bs_read_weights(const bs_stage *stage, uint64_t offset, uint64_t count, float *out);
@@ -179,8 +178,7 @@ int bs_read_weights(const bs_stage *stage, uint64_t offset, uint64_t count, floa
 int bs_prompt_ids(uint64_t seed, int32_t n, int32_t vocab, int32_t *out);
 
 /* Profiling: time every launch of one kernel class with HIP events on the stage stream.
- * kernel_class: 0 off, 1 weight GEMV (decode), 2 GEMM (prefill), 3 attention,
- *   4 persistent decode step (one launch per step; bytes = the step's algorithmic HBM bytes).
+ * kernel_class: 0 off, 1 weight GEMV (decode), 2 GEMM (prefill), 3 attention.
  * bs_profile_read returns accumulated milliseconds, launch count and algorithmic bytes
  * (or flops for class 2) since the last bs_profile_enable; it synchronizes the stream. */
 int bs_profile_enable(bs_stage *stage, int32_t kernel_class);

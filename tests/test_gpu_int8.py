@@ -11,7 +11,7 @@ from distributed_inference_demo_amd.stage import Stage
 from oracle import gen_np
 from oracle.oracle import OracleStage
 
-from test_gpu_parity import canonical_weights, check_close
+from test_gpu_parity import assert_ids_match, canonical_weights, check_close
 
 pytestmark = pytest.mark.gpu
 
@@ -84,14 +84,15 @@ def test_int8_batched_greedy_decode(B):
     h, nh, L, V = 512, 8, 3, 2048
     gs, os_ = pair8(h, nh, L, V, 0, L, seed=7, max_batch=B + 1, max_ctx=40, max_tokens=B * 8)
     ids = gen_np.prompt_ids(9, B, 8, V).astype(np.int32)
-    tg = gs.forward_host(ids, B, 8, slot=1, past_len=0)
-    to = os_.forward(ids, B, 8, slot=1, past_len=0)
+    tg, lg = gs.forward_host(ids, B, 8, slot=1, past_len=0, want_logits=True)
+    to, lo = os_.forward(ids, B, 8, slot=1, past_len=0, want_logits=True)
+    check_close(lg, lo, "bf16", f"B={B} int8 prefill")
+    assert_ids_match(tg, to, lo, f"B={B} int8 prefill")
     for step in range(6):
-        assert np.mean(tg == to) >= 0.9, (step, tg, to)
-        tg_n, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=1, past_len=8 + step, want_logits=True)
-        to_n, lo = os_.forward(to.reshape(B, 1), B, 1, slot=1, past_len=8 + step, want_logits=True)
+        tg, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=1, past_len=8 + step, want_logits=True)
+        to, lo = os_.forward(to.reshape(B, 1), B, 1, slot=1, past_len=8 + step, want_logits=True)
         check_close(lg, lo, "bf16", f"B={B} int8 decode step {step}")
-        tg, to = tg_n, to_n
+        assert_ids_match(tg, to, lo, f"B={B} int8 decode step {step}")
 
 
 def test_int8_long_context_graph_decode():
@@ -122,22 +123,19 @@ def test_int8_long_context_graph_decode():
 
 def test_serve_run_int8_on_gpu_matches_oracle():
     """serve.py lifecycle on one GPU with an int8 model (bf16 stage, BS_FLAG_INT8_WEIGHTS): 4 samples,
-    2 in flight; each sample's greedy ids against the int8 oracle decoding it alone (bf16 noise may
-    flip a near-tie later in a sequence: the first id must match, 80 % of all ids)."""
+    2 in flight; each sample's greedy ids against the int8 oracle decoding it alone, teacher-forced
+    with the served ids: every id equal unless the oracle's top-2 margin at that step is < 2e-2."""
     import torch
     from distributed_inference_demo_amd.config import BloomDims
     from distributed_inference_demo_amd.serve import RunConfig, run_rank, synthetic_prompts
     model = BloomDims("tinygpu-int8", 256, 2, 4, vocab=1024, int8_weights=True)
     cfg = RunConfig(model=model, num_sample=4, max_length=8, core_pool_size=2, prompt_len=9, dtype="bf16", seed=13)
     res = run_rank(cfg, 0, 1, torch.device("cuda", 0))
-    agree = []
     for got, p in zip(res["samples"], synthetic_prompts(cfg, model.vocab)):
         o = OracleStage(256, 4, 2, 1024, 0, 2, bf16=True, max_batch=1, max_ctx=32, seed=13, int8=True)
-        tok = o.forward(np.array(p, np.int32).reshape(1, -1), 1, len(p))
-        ids = [int(tok[0])]
+        tok, lo = o.forward(np.array(p, np.int32).reshape(1, -1), 1, len(p), want_logits=True)
+        assert_ids_match([got[0]], tok, lo, "int8 serve first id")
         for i in range(cfg.max_length - 1):
-            tok = o.forward(np.array([[got[i]]], np.int32), 1, 1, past_len=len(p) + i)  # teacher-forced
-            ids.append(int(tok[0]))
-        assert got[0] == ids[0]
-        agree += [a == b for a, b in zip(got, ids)]
-    assert np.mean(agree) >= 0.8
+            tok, lo = o.forward(np.array([[got[i]]], np.int32), 1, 1, past_len=len(p) + i,  # teacher-forced
+                                want_logits=True)
+            assert_ids_match([got[i + 1]], tok, lo, f"int8 serve id {i + 1}")

@@ -48,6 +48,16 @@ def check_close(got, ref, dtype, what=""):
     return err
 
 
+def assert_ids_match(got, ref_ids, ref_logits, what="", tol=BF16_TOL):
+    """Greedy ids equal to the checker's, except rows whose checker top-2 logit margin is < tol
+    (a near-tie inside the bf16 tolerance may legitimately pick either token)."""
+    got, ref_ids = np.asarray(got).reshape(-1), np.asarray(ref_ids).reshape(-1)
+    ref_logits = np.asarray(ref_logits).reshape(len(ref_ids), -1)
+    for b in np.flatnonzero(got != ref_ids):
+        top2 = np.sort(ref_logits[b])[-2:]
+        assert top2[1] - top2[0] < tol, f"{what}: row {b} id {got[b]} != {ref_ids[b]}, checker top-2 {top2}"
+
+
 def test_tiny_fp32_matches_hf_golden_and_greedy_128():
     g = np.load(os.path.join(G, "tiny_e2e.npz"))
     h, nh, L, V, seed, B, S = (int(v) for v in g["config"])
@@ -109,14 +119,15 @@ def test_batched_decode_with_slot_offset(B):
     h, nh, L, V = 256, 4, 2, 1024
     gs, os_ = pair(h, nh, L, V, 0, L, "bf16", seed=3, max_batch=B + 2, max_ctx=40, max_tokens=B * 8)
     ids = gen_np.prompt_ids(5, B, 8, V).astype(np.int32)
-    tg = gs.forward_host(ids, B, 8, slot=2, past_len=0)
-    to = os_.forward(ids, B, 8, slot=2, past_len=0)
+    tg, lg = gs.forward_host(ids, B, 8, slot=2, past_len=0, want_logits=True)
+    to, lo = os_.forward(ids, B, 8, slot=2, past_len=0, want_logits=True)
+    check_close(lg, lo, "bf16", "prefill")
+    assert_ids_match(tg, to, lo, "prefill")
     for step in range(4):
-        assert np.mean(tg == to) >= 0.9, (step, tg, to)
-        tg_n, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=2, past_len=8 + step, want_logits=True)
-        to_n, lo = os_.forward(to.reshape(B, 1), B, 1, slot=2, past_len=8 + step, want_logits=True)
+        tg, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=2, past_len=8 + step, want_logits=True)
+        to, lo = os_.forward(to.reshape(B, 1), B, 1, slot=2, past_len=8 + step, want_logits=True)
         check_close(lg, lo, "bf16", f"decode step {step}")
-        tg, to = tg_n, to_n
+        assert_ids_match(tg, to, lo, f"decode step {step}")
 
 
 @pytest.mark.parametrize("B", [8, 32])
@@ -132,7 +143,7 @@ def test_batched_decode_real_width_split_k(B):
         tg_n, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=0, past_len=4 + step, want_logits=True)
         to_n, lo = os_.forward(to.reshape(B, 1), B, 1, slot=0, past_len=4 + step, want_logits=True)
         check_close(lg, lo, "bf16", f"B={B} decode step {step}")
-        assert np.mean(tg_n == to_n) >= 0.9, (step, tg_n, to_n)
+        assert_ids_match(tg_n, to_n, lo, f"B={B} decode step {step}")
         tg, to = tg_n, to_n
 
 
