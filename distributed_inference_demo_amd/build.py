@@ -43,7 +43,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     bid = source_hash()
     old = open(STAMP).read().strip() if os.path.exists(STAMP) else ""
-    force = force or old != bid
+    restamp = old != bid  # only stage.hip carries the stamp
     hdr_t = max([_mtime(os.path.join(CSRC, h)) for h in HEADERS] + [_mtime(os.path.join(ROOT, "include", "bloomstage.h"))])
     jobs = []
     objs = []
@@ -51,7 +51,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         sp = os.path.join(CSRC, src)
         op = os.path.join(OBJ, src + ".o")
         objs.append(op)
-        if force or _mtime(op) < max(_mtime(sp), hdr_t):
+        if force or (restamp and src == "stage.hip") or _mtime(op) < max(_mtime(sp), hdr_t):
             flags = list(CFLAGS)
             if src.endswith(".cpp"):
                 flags = [f for f in flags if not f.startswith("--offload-arch")] + ["-x", "c++"]

@@ -11,6 +11,7 @@
 // reference's silent stream desynchronisation (utils.cpp:244-246, :359-361).
 // A zero-tensor-count buffer is legal (8 bytes).  Deserialisation never copies: views point
 // into the caller's byte buffer (the reference copies 4-6 times per hop).
+#include <cstdint>
 #include <cstring>
 
 #include "../../include/bloomstage.h"
@@ -37,7 +38,9 @@ static bool elem_count(const bs_tensor_view& t, uint64_t* n) {
   uint64_t c = 1;
   for (int i = 0; i < t.ndim; i++) {
     if (t.dims[i] < 0) return false;
-    c *= (uint64_t)t.dims[i];
+    const uint64_t d = (uint64_t)t.dims[i];
+    if (d && c > UINT64_MAX / d) return false;  // a crafted wire shape must not wrap the count
+    c *= d;
   }
   *n = c;
   return true;
@@ -52,6 +55,7 @@ extern "C" int64_t bs_codec_serialize(const bs_tensor_view* tensors, int32_t n, 
     uint64_t cnt;
     if (!elem_count(tensors[i], &cnt)) return BS_ERR_INVALID;
     if (cnt && !tensors[i].data) return BS_ERR_INVALID;
+    if (cnt > (UINT64_MAX / 2 - total) / (uint64_t)es) return BS_ERR_INVALID;
     total += 4 + 8 + 8ull * tensors[i].ndim + cnt * (uint64_t)es;
   }
   if (!out || cap < total) return (int64_t)total;
@@ -101,8 +105,8 @@ extern "C" int bs_codec_deserialize(const void* bytes, uint64_t len, bs_tensor_v
     if (es < 0) return BS_ERR_UNSUPPORTED;
     uint64_t cnt;
     if (!elem_count(v, &cnt)) return BS_ERR_INVALID;
+    if (cnt > (uint64_t)(end - p) / (uint64_t)es) return BS_ERR_INVALID;  // before cnt * es can wrap
     const uint64_t nb = cnt * (uint64_t)es;
-    if ((uint64_t)(end - p) < nb) return BS_ERR_INVALID;
     v.data = p;
     p += nb;
     if ((int64_t)i < max_views && views) views[i] = v;

@@ -233,6 +233,13 @@ def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb
     tied lm_head when head_split) and its Pipeline.  Collective: every rank must call it."""
     head_split = (world > 1) if head_split is None else (head_split and world > 1)
     n_mb = (2 * world if head_split else world) if n_mb is None else n_mb
+    if world > model.n_layer:
+        raise ValueError(f"{world} stages for {model.n_layer} layers: every stage needs at least one layer")
+    if head_split and world > model.vocab // 16:
+        raise ValueError(f"vocabulary-parallel head: {world} slices of a {model.vocab}-token vocabulary "
+                         "leave a slice without a 16-column tile")
+    if model.int8_weights and dtype != "bf16":
+        raise ValueError(f"{model.name}: weight-only int8 stages need dtype bf16 (got {dtype})")
     lb, le = stage_ranges(world, model.n_layer)[rank]
     is_first, is_last = rank == 0, rank == world - 1
     hslice = vocab_slices(model.vocab, world)[rank] if head_split else None
@@ -241,8 +248,7 @@ def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb
         st = Stage(model.hidden, model.n_head, model.n_layer, model.vocab, lb, le, dtype=dtype,
                    device=device.index if device.type == "cuda" else 0, max_batch=mb_rows * n_mb,
                    max_ctx=max_ctx, max_tokens=mb_rows * max_seq, seed=seed, is_first=is_first,
-                   is_last=is_last and not head_split, head_slice=hslice,
-                   int8_weights=model.int8_weights and dtype == "bf16")
+                   is_last=is_last and not head_split, head_slice=hslice, int8_weights=model.int8_weights)
         ex = StageExecutor(st)
     else:
         ex = executor_factory(lb, le, is_first, is_last and not head_split, mb_rows * n_mb, max_ctx, hslice)

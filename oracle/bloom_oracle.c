@@ -186,6 +186,10 @@ static inline float rb(const or_stage *s, float v) { return s->bf16 ? gen_bf16_r
 
 static int g_accum_double = 0; /* test knob: accumulate dot products in double */
 void or_set_accum_double(int on) { g_accum_double = on; }
+/* diagnostic knob: bits of bf16 rounding points to SKIP (1 LN out, 2 K/V, 4 q, 8 ctx, 16 GELU out) */
+static int g_skip_round = 0;
+void or_set_skip_round(int mask) { g_skip_round = mask; }
+static inline float rbp(const or_stage *s, int point, float v) { return (g_skip_round & point) ? v : rb(s, v); }
 
 static float dotf(const float *a, const float *b, int K) {
   if (g_accum_double) {
@@ -219,7 +223,7 @@ static void layernorm(const float *x, float *y, int M, int K, const float *g, co
     float mf = (float)mean;
     for (int k = 0; k < K; k++) {
       float v = (xr[k] - mf) * rstd * g[k] + b[k];
-      y[(size_t)m * K + k] = round_out ? rb(s, v) : v;
+      y[(size_t)m * K + k] = round_out ? rbp(s, 1, v) : v;
     }
   }
 }
@@ -281,7 +285,7 @@ int or_forward(or_stage *s, int B, int S, int slot, int past_len, const void *in
       for (int hh = 0; hh < nh; hh++) {
         const float *base = qkv + (size_t)m * 3 * h + (size_t)hh * 3 * hd;
         float *kd = kv_ptr(s, li, 0, slot + b, hh, pos), *vd = kv_ptr(s, li, 1, slot + b, hh, pos);
-        for (int d = 0; d < hd; d++) { kd[d] = rb(s, base[hd + d]); vd[d] = rb(s, base[2 * hd + d]); }
+        for (int d = 0; d < hd; d++) { kd[d] = rbp(s, 2, base[hd + d]); vd[d] = rbp(s, 2, base[2 * hd + d]); }
       }
     }
 #pragma omp parallel for collapse(2) schedule(dynamic)
@@ -293,7 +297,7 @@ int or_forward(or_stage *s, int B, int S, int slot, int past_len, const void *in
           int m = b * S + t, nk = past_len + t + 1; /* causal: keys 0..pos */
           const float *q0 = qkv + (size_t)m * 3 * h + (size_t)hh * 3 * hd;
           float q[256];  /* the device stores q in the activation dtype (bf16 mode: rounded) */
-          for (int d = 0; d < hd; d++) q[d] = rb(s, q0[d]);
+          for (int d = 0; d < hd; d++) q[d] = rbp(s, 4, q0[d]);
           float mx = -INFINITY;
           for (int j = 0; j < nk; j++) {
             float qk = dotf(q, kv_ptr(s, li, 0, slot + b, hh, j), hd);
@@ -311,7 +315,7 @@ int or_forward(or_stage *s, int B, int S, int slot, int past_len, const void *in
             float p = sc[j] * inv;
             for (int d = 0; d < hd; d++) o[d] += p * vr[d];
           }
-          for (int d = 0; d < hd; d++) o[d] = rb(s, o[d]);
+          for (int d = 0; d < hd; d++) o[d] = rbp(s, 8, o[d]);
         }
         free(sc);
       }
@@ -320,7 +324,7 @@ int or_forward(or_stage *s, int B, int S, int slot, int past_len, const void *in
     for (size_t i = 0; i < (size_t)M * h; i++) a[i] = a[i] + x[i];
     layernorm(a, xn, M, h, w->ln2_g, w->ln2_b, s->eps, 1, s);
     linear(xn, w->fc1_w, w->fc1_b, g, M, 4 * h, h);
-    for (size_t i = 0; i < (size_t)M * 4 * h; i++) g[i] = rb(s, gelu_bloom(g[i]));
+    for (size_t i = 0; i < (size_t)M * 4 * h; i++) g[i] = rbp(s, 16, gelu_bloom(g[i]));
     linear(g, w->fc2_w, w->fc2_b, x, M, h, 4 * h);
     for (size_t i = 0; i < (size_t)M * h; i++) x[i] = x[i] + a[i];
   }

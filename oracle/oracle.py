@@ -28,6 +28,7 @@ def lib():
         L.or_read_kv.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p]
         L.or_num_threads.restype = ctypes.c_int
         L.or_set_accum_double.argtypes = [ctypes.c_int]
+        L.or_set_skip_round.argtypes = [ctypes.c_int]
         L.or_quantize_int8.restype = ctypes.c_int
         L.or_quantize_int8.argtypes = [ctypes.c_void_p]
         L.or_head_norm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]

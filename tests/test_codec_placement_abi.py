@@ -57,6 +57,16 @@ def test_codec_empty_vector_and_errors():
         bs.deserialize_int(b"\x01\x02\x03")
 
 
+@pytest.mark.parametrize("dims", [(2 ** 62, 4), (2 ** 32, 2 ** 32), (2 ** 63 - 1, 2 ** 63 - 1, 2)])
+def test_codec_rejects_wrapping_wire_shapes(dims):
+    """A crafted header whose element count (or count x element size) wraps uint64 must be rejected,
+    not handed back as a view whose dims describe more bytes than the buffer holds."""
+    hdr = (1).to_bytes(8, "little") + (1).to_bytes(4, "little") + len(dims).to_bytes(8, "little")
+    hdr += b"".join(int(d).to_bytes(8, "little") for d in dims)
+    with pytest.raises(bs.BloomStageError):
+        bs.deserialize_tensors(hdr + bytes(16))
+
+
 @pytest.mark.parametrize("dev,mods", [(1, 24), (2, 24), (4, 30), (8, 30), (3, 2), (2, 2), (5, 3)])
 def test_round_robin_matches_reference_semantics(dev, mods):
     arr = round_robin_module_arrangement(dev, mods)

@@ -4,12 +4,15 @@ fixtures.
 
 Tolerances (BASELINE.json north_star):
   fp32 mode: max|gpu - ref| <= 1e-3 * max|ref| (relative 1e-3), and identical greedy ids.
-  bf16 mode: max|gpu - ref| <= max(2e-2, 2.5e-3 * max|ref|) (ref = oracle with the same bf16
-             storage roundings).  The 2e-2 floor is the north-star bound; it scales with the
-             output magnitude because the bf16 roundings of GEMM inputs flip with accumulation
-             order: two fp32 accumulation orders of the SAME bf16-emulated math differ by
-             0.0177 max-abs on one bloom-7b1 block whose outputs reach 12.1
-             (tests/test_oracle_golden.py::test_bf16_noise_floor_of_the_checker).
+  bf16 mode: logits max|gpu - ref| <= 2e-2 (north_star) where |logits| <= 8; hidden states
+             max|gpu - ref| <= 2e-2 + 2^-9 * max|ref| (ref = oracle with the same bf16 storage
+             roundings): the north-star 2e-2 plus half a bf16 ulp of the largest output.  The extra
+             term matters only for wide blocks (bloom-3b/7b1, outputs up to 13): there every
+             intermediate rounded to bf16 (LayerNorm out, q/K/V, attention context, GELU out) flips with
+             the accumulation order of the sums that produce it, and the flips spread over the whole
+             row.  A float64 restatement of the same rounded math lands 0.011 max / 0.0021 mean from
+             the fp32 checker on a bloom-7b1-width block and the GPU 0.017 / 0.0034 (tools/diag_parity.py,
+             DESIGN.md section 2): the error is the rounding noise of the format, not of the kernels.
 """
 import os
 
@@ -17,6 +20,7 @@ import numpy as np
 import pytest
 
 from distributed_inference_demo_amd.stage import (BloomStageError, Stage, create_session, deserialize_int,
+                                                  deserialize_tensors,
                                                   run_inference_master_residual, run_inference_worker_residual,
                                                   run_inference_worker_residual_last_generation)
 from distributed_inference_demo_amd.config import BloomDims
@@ -40,8 +44,19 @@ def pair(h, nh, L, V, lb, le, dtype, seed=0, max_batch=1, max_ctx=128, max_token
 def check_close(got, ref, dtype, what=""):
     err = float(np.abs(got - ref).max())
     if dtype == "bf16":
-        tol = max(BF16_TOL, 2.5e-3 * float(np.abs(ref).max()))
+        tol = BF16_TOL + 2.0 ** -9 * float(np.abs(ref).max())
         assert err <= tol, f"{what}: max-abs {err} > {tol}"
+    else:
+        scale = float(np.abs(ref).max())
+        assert err <= FP32_REL * scale, f"{what}: max-abs {err} > {FP32_REL} * {scale}"
+    return err
+
+
+def check_logits(got, ref, dtype, what=""):
+    """Logits: north_star's flat 2e-2 max-abs in bf16 (relative 1e-3 in fp32)."""
+    err = float(np.abs(got - ref).max())
+    if dtype == "bf16":
+        assert err <= BF16_TOL, f"{what}: logits max-abs {err} > {BF16_TOL}"
     else:
         scale = float(np.abs(ref).max())
         assert err <= FP32_REL * scale, f"{what}: max-abs {err} > {FP32_REL} * {scale}"
@@ -63,7 +78,7 @@ def test_tiny_fp32_matches_hf_golden_and_greedy_128():
     h, nh, L, V, seed, B, S = (int(v) for v in g["config"])
     st = Stage(h, nh, L, V, 0, L, dtype="fp32", max_batch=B, max_ctx=S + 128, seed=seed)
     tok, lg = st.forward_host(g["ids"], B, S, want_logits=True)
-    check_close(lg, g["logits"], "fp32", "tiny logits vs HF")
+    check_logits(lg, g["logits"], "fp32", "tiny logits vs HF")
     toks = [tok]
     for i in range(127):
         toks.append(st.forward_host(toks[-1].reshape(B, 1), B, 1))
@@ -84,7 +99,7 @@ def test_tiny_stage_splits_match_oracle(dtype):
             check_close(hid_g, g["layer_out"][split - 1], dtype, "stage0 vs HF")
         tg, lg = g1.forward_host(hid_o, B, S, want_logits=True)
         to, lo = o1.forward(hid_o, B, S, want_logits=True)
-        check_close(lg, lo, dtype, "stage1 logits")
+        check_logits(lg, lo, dtype, "stage1 logits")
         assert np.array_equal(tg, to)
 
 
@@ -121,12 +136,12 @@ def test_batched_decode_with_slot_offset(B):
     ids = gen_np.prompt_ids(5, B, 8, V).astype(np.int32)
     tg, lg = gs.forward_host(ids, B, 8, slot=2, past_len=0, want_logits=True)
     to, lo = os_.forward(ids, B, 8, slot=2, past_len=0, want_logits=True)
-    check_close(lg, lo, "bf16", "prefill")
+    check_logits(lg, lo, "bf16", "prefill")
     assert_ids_match(tg, to, lo, "prefill")
     for step in range(4):
         tg, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=2, past_len=8 + step, want_logits=True)
         to, lo = os_.forward(to.reshape(B, 1), B, 1, slot=2, past_len=8 + step, want_logits=True)
-        check_close(lg, lo, "bf16", f"decode step {step}")
+        check_logits(lg, lo, "bf16", f"decode step {step}")
         assert_ids_match(tg, to, lo, f"decode step {step}")
 
 
@@ -142,7 +157,7 @@ def test_batched_decode_real_width_split_k(B):
     for step in range(3):
         tg_n, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=0, past_len=4 + step, want_logits=True)
         to_n, lo = os_.forward(to.reshape(B, 1), B, 1, slot=0, past_len=4 + step, want_logits=True)
-        check_close(lg, lo, "bf16", f"B={B} decode step {step}")
+        check_logits(lg, lo, "bf16", f"B={B} decode step {step}")
         assert_ids_match(tg_n, to_n, lo, f"B={B} decode step {step}")
         tg, to = tg_n, to_n
 
@@ -160,7 +175,7 @@ def test_nonpow2_heads_fp32_matches_hf():
     h, nh, L, V, seed, B, S = (int(v) for v in g["config"])
     st = Stage(h, nh, L, V, 0, L, dtype="fp32", max_batch=B, max_ctx=S, seed=seed)
     _, lg = st.forward_host(g["ids"], B, S, want_logits=True)
-    check_close(lg, g["logits"], "fp32", "nonpow2 logits vs HF")
+    check_logits(lg, g["logits"], "fp32", "nonpow2 logits vs HF")
 
 
 def canonical_weights(seed, h, L, V, lb=0, le=None, first=True, last=True):
@@ -225,6 +240,28 @@ def test_jni_mirror_entry_points_two_stage_loopback():
     assert toks == list(g["greedy"][0][:8])
 
 
+def test_jni_mirror_middle_entry_three_stage_loopback():
+    """Header -> middle (runInferenceWorkerResidual, native-lib.cpp:1036-1194) -> tail, every hop
+    as the utils.cpp wire bytes; greedy ids equal the HF golden fixture."""
+    m = BloomDims("tiny", 64, 4, 4, vocab=512)
+    g = np.load(os.path.join(G, "tiny_e2e.npz"))
+    head = create_session(m, 0, 1, dtype="fp32", max_ctx=64)
+    mid = create_session(m, 1, 3, dtype="fp32", max_ctx=64)
+    tail = create_session(m, 3, 4, dtype="fp32", max_ctx=64)
+    ids = list(g["ids"][0])
+    toks = []
+    seq, res = run_inference_master_residual(head, ids)
+    for _ in range(8):
+        seq2, res2 = run_inference_worker_residual(mid, seq, res)
+        assert res2 == []
+        (hid,) = deserialize_tensors(seq2)
+        assert hid.dtype == np.float32 and hid.shape[-1] == m.hidden
+        tok = deserialize_int(run_inference_worker_residual_last_generation(tail, seq2, res2, k=1))
+        toks.append(tok)
+        seq, res = run_inference_master_residual(head, [tok])
+    assert toks == list(g["greedy"][0][:8])
+
+
 def test_errors_are_status_codes_not_crashes():
     st = Stage(64, 4, 4, 512, 0, 4, dtype="bf16", max_ctx=8)
     with pytest.raises(BloomStageError, match="max_ctx"):
@@ -254,14 +291,14 @@ def test_graph_replayed_decode_matches_oracle_long_context(dtype):
         gs.forward(tin, tok, B, P, slot=0, past_len=0, logits=lg, stream=cs.cuda_stream)
         to, lo = os_.forward(ids, B, P, want_logits=True)
         torch.cuda.synchronize()
-        check_close(lg.cpu().numpy(), lo, dtype, "prefill logits")
+        check_logits(lg.cpu().numpy(), lo, dtype, "prefill logits")
         for step in range(130):
             tok.copy_(torch.from_numpy(to))  # teacher-force the oracle's tokens
             gs.forward(tok, tok, B, 1, slot=0, past_len=P + step, logits=lg, stream=cs.cuda_stream)
             to, lo = os_.forward(to.reshape(B, 1), B, 1, past_len=P + step, want_logits=True)
             if step % 13 == 0 or step == 129:
                 torch.cuda.synchronize()
-                check_close(lg.cpu().numpy(), lo, dtype, f"decode step {step} (ctx {P + step + 1})")
+                check_logits(lg.cpu().numpy(), lo, dtype, f"decode step {step} (ctx {P + step + 1})")
 
 
 def test_graph_and_eager_paths_agree_bitwise():
@@ -345,7 +382,7 @@ def test_small_batch_decode_from_empty_cache(B, slot, hd):
             to_next, lo = os_.forward(to.reshape(B, 1), B, 1, past_len=past, slot=slot, want_logits=True)
             if step in steps:
                 torch.cuda.synchronize()
-                check_close(lg.cpu().numpy(), lo, "bf16", f"fused decode step {step} (ctx {past + 1})")
+                check_logits(lg.cpu().numpy(), lo, "bf16", f"fused decode step {step} (ctx {past + 1})")
             to = to_next
             past += 1
 

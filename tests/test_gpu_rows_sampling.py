@@ -18,7 +18,7 @@ from oracle import gen_np
 from oracle.oracle import OracleStage
 from oracle.sampling_ref import sample_pick, topk_reference_order
 
-from test_gpu_parity import BF16_TOL, assert_ids_match, canonical_weights, check_close
+from test_gpu_parity import BF16_TOL, assert_ids_match, canonical_weights, check_close, check_logits
 
 pytestmark = pytest.mark.gpu
 
@@ -42,7 +42,7 @@ def test_rows_at_different_positions_match_per_row_checker(dtype):
     tg, lg = g.forward_host(chunk, B, 5, slot=0, past_len=past, want_logits=True)
     for r in range(B):
         to, lo = o.forward(chunk[r:r + 1], 1, 5, slot=r, past_len=past[r], want_logits=True)
-        check_close(lg[r:r + 1], lo, dtype, f"row {r} chunk at position {past[r]}")
+        check_logits(lg[r:r + 1], lo, dtype, f"row {r} chunk at position {past[r]}")
         assert_ids_match(tg[r:r + 1], to, lo, f"row {r} chunk")
         toks[r] = to
     past = [p + 5 for p in past]
@@ -51,7 +51,7 @@ def test_rows_at_different_positions_match_per_row_checker(dtype):
         tg, lg = g.forward_host(x, B, 1, slot=0, past_len=past, want_logits=True)
         for r in range(B):
             to, lo = o.forward(x[r:r + 1], 1, 1, slot=r, past_len=past[r], want_logits=True)
-            check_close(lg[r:r + 1], lo, dtype, f"step {step} row {r} (position {past[r]})")
+            check_logits(lg[r:r + 1], lo, dtype, f"step {step} row {r} (position {past[r]})")
             assert_ids_match(tg[r:r + 1], to, lo, f"step {step} row {r}")
             toks[r] = to
         past = [p + 1 for p in past]
@@ -88,7 +88,7 @@ def test_rows_at_different_positions_graph_replay():
             for r in range(B):
                 to, lo = o.forward(x[r:r + 1].reshape(1, 1), 1, 1, slot=r, past_len=past[r], want_logits=True)
                 if step % 6 == 0 or step == 39:
-                    check_close(gl[r:r + 1], lo, "bf16", f"graph step {step} row {r}")
+                    check_logits(gl[r:r + 1], lo, "bf16", f"graph step {step} row {r}")
                 assert_ids_match(gt[r:r + 1], to, lo, f"graph step {step} row {r}")
                 toks[r] = to
             past = [p + 1 for p in past]
@@ -205,7 +205,7 @@ def test_head_norm_and_slice_match_checker(dtype):
         # the key's high word is the order-preserving image of the winning logit
         gv = _key_value(got_keys)
         wv = _key_value(want_keys)
-        check_close(gv, wv, dtype, f"head_slice {i} max logit")
+        check_logits(gv, wv, dtype, f"head_slice {i} max logit")
         keys = want_keys  # the ring carries the checker's keys on (each hop checked on its own)
     _, full = o.forward(hidden, B, S, want_logits=True)
     assert_ids_match(tk.cpu().numpy(), np.argmax(full, axis=1), full, "ring token", tol=BF16_TOL)

@@ -93,6 +93,19 @@ def test_pipeline_matches_single_stage(world, head_split):
     assert np.array_equal(got, np.stack(want, 1))
 
 
+def test_build_rank_rejects_unplaceable_splits():
+    """More stages than layers (an empty stage), more head slices than 16-column tiles, and an
+    int8 model in fp32 are configuration errors, raised before any stage is built."""
+    cpu = torch.device("cpu")
+    with pytest.raises(ValueError, match="at least one layer"):
+        build_rank(MODEL, 0, MODEL.n_layer + 1, cpu, executor_factory=OracleExecutor, dtype="fp32")
+    narrow = config.BloomDims("narrow", 64, 8, 4, vocab=64)
+    with pytest.raises(ValueError, match="16-column tile"):
+        build_rank(narrow, 0, 5, cpu, executor_factory=OracleExecutor, dtype="fp32", head_split=True)
+    with pytest.raises(ValueError, match="int8"):
+        build_rank(config.get("bloom560m-int8"), 0, 1, cpu, executor_factory=OracleExecutor, dtype="fp32")
+
+
 def test_single_rank_pipeline_loops_tokens_back():
     pipe, _ = build_rank(MODEL, 0, 1, torch.device("cpu"), mb_rows=MB, n_mb=2, max_ctx=P + STEPS + 2, max_seq=P,
                          executor_factory=OracleExecutor, dtype="fp32")
