@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--weights", default="bf16", choices=["bf16", "int8"],
                    help="int8: weight-only int8 block matrices (BS_FLAG_INT8_WEIGHTS, the bloom*-int8 variants)")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU checker on a bounded sample")
-    p.add_argument("--cpu-steps", type=int, default=12)
+    p.add_argument("--cpu-steps", type=int, default=24)
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     p.add_argument("--no-head-split", action="store_true", help="pipeline: keep the whole lm_head on the last stage")
@@ -83,29 +83,115 @@ def pmc_traffic(args, kernel_tag, timeout=240):
     return tot["FETCH_SIZE"][0] + tot["WRITE_SIZE"][0], tot["FETCH_SIZE"][1]
 
 
-def cpu_baseline(model, steps, seed):
-    """The oracle (C fp32 restatement, OpenMP over the host cores) timed on a bounded sample:
-    KV-cached decode of `steps` tokens after a 16-token prompt, same model, same generator."""
+def _host_info():
+    import platform
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": _cpu_model(), "machine": platform.machine()}
+
+
+def _cpu_stages(model, ranges, n_ctx, seed):
+    from oracle.oracle import OracleStage
+    return [OracleStage(model.hidden, model.n_head, model.n_layer, model.vocab, a, b, bf16=False, max_batch=1,
+                        max_ctx=n_ctx, seed=seed, is_first=(a == 0), is_last=(b == model.n_layer))
+            for a, b in ranges]
+
+
+def _run_cpu_stages(model, stages, prompt, steps, mode, warmup=3):
+    """The reference's CPU execution model on the C restatement (oracle/bloom_oracle.c, fp32, OpenMP):
+    one stage object per layer range, every hop serialized in the utils.cpp wire format
+    (SerializeTensorVectorToBytes / DeserializeTensorVectorFromBytes, utils.cpp:124-368, here bs_codec_*),
+    greedy tokens.  mode "cpu-kv": KV-cached decode; "cpu-ref": every token recomputes the whole
+    sequence without a cache (what the reference's input_ids-only ONNX modules compute,
+    Communication.java:322-326).  Returns tokens/s over `steps` timed tokens."""
     import numpy as np
-    from oracle.oracle import OracleStage, num_threads, prompt_ids
+    from distributed_inference_demo_amd.stage import deserialize_tensors, serialize_tensors
+    from oracle.oracle import prompt_ids
+    seq = [int(t) for t in prompt_ids(1234, 1, prompt, model.vocab).reshape(-1)]
+
+    def token(ids, past):
+        x = np.asarray(ids, np.int32).reshape(1, -1)
+        S = x.shape[1]
+        for st in stages:
+            y = st.forward(x, 1, S, past_len=past)
+            if not st.is_last:
+                (x,) = deserialize_tensors(serialize_tensors([y]))  # the inter-stage hop
+        return int(y[0])
+
+    if mode == "cpu-kv":
+        tok = token(seq, 0)
+        seq.append(tok)
+        for _ in range(warmup):
+            tok = token([tok], len(seq) - 1)
+            seq.append(tok)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            tok = token([tok], len(seq) - 1)
+            seq.append(tok)
+    else:
+        for _ in range(1 + warmup):
+            seq.append(token(seq, 0))
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            seq.append(token(seq, 0))
+    return steps / (time.perf_counter() - t0)
+
+
+def cpu_baseline(model, steps, seed, ranges=None):
+    """Host-CPU baseline of the same run (BASELINE.md "CPU baseline plan"): the fp32 C restatement on a
+    bounded sample of the benchmarked model and stage split (cpu-kv: `steps` tokens, cpu-ref: a few),
+    plus BASELINE.json configs[0] (bloom-560m, 2 stages [0,12) [12,24), wire-format loopback).  Prompts
+    are 16 tokens (a 512-token CPU prefill alone would take minutes; the per-token cost of a cached
+    decode changes by < 3 % of its FLOPs between 16 and 512 positions), 3 warm-up tokens excluded."""
+    from distributed_inference_demo_amd import config
+    from distributed_inference_demo_amd.placement import stage_ranges
+    from oracle.oracle import num_threads
+    ranges = ranges or [(0, model.n_layer)]
+    n_ref, n_ctx = max(2, steps // 6), 16 + 3 + steps + 4
     t0 = time.perf_counter()
-    st = OracleStage(model.hidden, model.n_head, model.n_layer, model.vocab, 0, model.n_layer, bf16=False,
-                     max_batch=1, max_ctx=16 + steps + 8, seed=seed)
+    st = _cpu_stages(model, ranges, n_ctx, seed)
     t_init = time.perf_counter() - t0
-    ids = prompt_ids(1234, 1, 16, model.vocab)
-    tok = st.forward(ids, 1, 16)
-    for i in range(2):  # warm-up tokens
-        tok = st.forward(tok.reshape(1, 1), 1, 1, past_len=16 + i)
-    t0 = time.perf_counter()
-    for i in range(steps):
-        tok = st.forward(tok.reshape(1, 1), 1, 1, past_len=18 + i)
-    dt = time.perf_counter() - t0
-    st.close()
-    return {"value": steps / dt, "unit": "tokens/s", "cores": num_threads(), "kind": "port",
-            "sample": f"{model.name} fp32 oracle (oracle/bloom_oracle.c), 1 stage, batch 1, KV-cached decode of "
-                      f"{steps} tokens after a 16-token prompt (+2 warm-up), {num_threads()} OpenMP threads; "
-                      f"weight generation {t_init:.1f}s excluded",
-            "cpu_model": _cpu_model()}
+    kv = _run_cpu_stages(model, st, 16, steps, "cpu-kv")
+    ref = _run_cpu_stages(model, st, 16, n_ref, "cpu-ref")
+    del st
+    m560 = config.get("bloom-560m")
+    r560 = stage_ranges(2, m560.n_layer)
+    st = _cpu_stages(m560, r560, n_ctx, seed)
+    kv560 = _run_cpu_stages(m560, st, 16, steps, "cpu-kv")
+    ref560 = _run_cpu_stages(m560, st, 16, max(2, steps // 4), "cpu-ref")
+    del st
+    host = _host_info()
+    return {"value": kv, "unit": "tokens/s", "cores": num_threads(), "kind": "port",
+            "sample": f"{model.name} fp32 C restatement (oracle/bloom_oracle.c), stages {ranges} joined by the "
+                      f"utils.cpp wire format, batch 1, cpu-kv: {steps} decode tokens after a 16-token prompt "
+                      f"(3 warm-up tokens excluded), {num_threads()} OpenMP threads; weight generation {t_init:.1f}s "
+                      "excluded",
+            "modes": {"cpu-kv": kv, "cpu-ref": ref},
+            "configs0_bloom560m_2stage_loopback": {"stages": r560, "cpu-kv": kv560, "cpu-ref": ref560,
+                                                   "unit": "tokens/s", "prompt": 16},
+            **host}
+
+
+def hbm_measured(dev):
+    """STREAM-like HBM figures on this GPU (report measured beside vendor peaks):
+    copy = torch copy_ of a 2 GiB buffer (read + write bytes / time), HIP events, best of 10."""
+    import torch
+    n = 1 << 30
+    a = torch.empty(n, dtype=torch.bfloat16, device=dev).fill_(1)
+    b = torch.empty_like(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = 1e9
+    for _ in range(12):
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    del a, b
+    torch.cuda.empty_cache()
+    return {"copy_GBps": 2 * 2 * n / (best * 1e-3) / 1e9, "method": "torch copy_ 2 GiB bf16, best of 12, HIP events"}
 
 
 def _cpu_model():
@@ -218,6 +304,12 @@ def bench_single(args):
         res["prefill"]["gemm_TFLOPs"] = pf_flops / (pf_ms * 1e-3) / 1e12
         res["prefill"]["gemm_frac_of_peak"] = res["prefill"]["gemm_TFLOPs"] / BF16_PEAK_TFLOPS
     st.close()
+    hbm = hbm_measured(dev)
+    res["hbm_measured"] = dict(hbm, vendor_peak_GBps=HBM_PEAK_GBPS)
+    if "roofline" in res:
+        res["roofline"]["peak_measured_copy"] = hbm["copy_GBps"]
+        res["roofline"]["frac_of_measured"] = res["roofline"]["achieved"] / hbm["copy_GBps"]
+    res["stage_hbm"]["frac_of_measured"] = res["stage_hbm"]["achieved_GBps"] / hbm["copy_GBps"]
     if args.cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(m, args.cpu_steps, args.seed)
     return res

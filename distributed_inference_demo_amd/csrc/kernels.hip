@@ -191,17 +191,29 @@ __device__ __forceinline__ void epi_store(const Epi& e, int m, int n, float v) {
 // output lane is known up front loads them at kernel start, so the epilogue is not one more memory
 // round trip after the reduction (decode GEMVs are latency-bound; each round trip is ~1 us).
 struct EpiPre {
-  float bias, resid;
+  uint32_t bias_bits;  // raw storage bits of bias[n] (bf16: low 16 bits), converted where used
+  float resid;
   int past;
 };
 
 template <typename T>
+__device__ __forceinline__ float bias_value(uint32_t bits) {
+  if constexpr (sizeof(T) == 2) return __uint_as_float(bits << 16);
+  else return __uint_as_float(bits);
+}
+
+// The loads go out unconditionally (lanes without an output read index 0) and stay raw until the
+// epilogue: a value converted here, or loaded under an exec-masked branch, makes the compiler wait
+// for it at once -- a whole HBM round trip before the weight stream is even issued.
+template <typename T>
 __device__ __forceinline__ EpiPre epi_prefetch(const Epi& e, int m, int n, bool valid) {
-  EpiPre p{0.f, 0.f, 0};
-  if (!valid || e.kind == EPI_ARGMAX) return p;
-  p.bias = to_f32(((const T*)e.bias)[n]);
-  if (e.kind == EPI_RESID) p.resid = e.resid[(size_t)m * e.ldo + n];
-  if (e.kind == EPI_QKV) p.past = e.past_dev ? e.past_dev[m / e.seq] : e.past;
+  EpiPre p{0u, 0.f, 0};
+  if (e.kind == EPI_ARGMAX) return p;  // uniform (kernel argument)
+  const int nn = valid ? n : 0, mm = valid ? m : 0;
+  if constexpr (sizeof(T) == 2) p.bias_bits = ((const unsigned short*)e.bias)[nn];
+  else p.bias_bits = ((const uint32_t*)e.bias)[nn];
+  if (e.kind == EPI_RESID) p.resid = e.resid[(size_t)mm * e.ldo + nn];
+  if (e.kind == EPI_QKV) p.past = e.past_dev ? e.past_dev[mm / e.seq] : e.past;
   return p;
 }
 
@@ -209,8 +221,9 @@ __device__ __forceinline__ EpiPre epi_prefetch(const Epi& e, int m, int n, bool 
 template <typename T, int KIND>
 __device__ __forceinline__ void epi_store_pre(const Epi& e, int m, int n, float v, const EpiPre& p) {
   if (e.col_scale) v *= e.col_scale[n];
+  const float bias = bias_value<T>(p.bias_bits);
   if constexpr (KIND == EPI_QKV) {
-    v += p.bias;
+    v += bias;
     const int three = 3 * e.head_dim;
     const int head = n / three, r = n - head * three, which = r / e.head_dim, d = r - which * e.head_dim;
     if (which == 0) {
@@ -222,9 +235,9 @@ __device__ __forceinline__ void epi_store_pre(const Epi& e, int m, int n, float 
       c[idx] = from_f32<T>(v);
     }
   } else if constexpr (KIND == EPI_RESID) {
-    e.out_f32[(size_t)m * e.ldo + n] = (v + p.bias) + p.resid;
+    e.out_f32[(size_t)m * e.ldo + n] = (v + bias) + p.resid;
   } else if constexpr (KIND == EPI_GELU) {
-    ((T*)e.out_act)[(size_t)m * e.ldo + n] = from_f32<T>(gelu_bloom(v + p.bias));
+    ((T*)e.out_act)[(size_t)m * e.ldo + n] = from_f32<T>(gelu_bloom(v + bias));
   }
 }
 
@@ -482,11 +495,13 @@ __device__ __forceinline__ void ln_rows_load(const LnArgs& ln, int M, int K, flo
   }
 }
 
+// Threads >= 256 of a wider block take no part (their loads were never issued) but pass the barriers.
 template <int MM>
 __device__ __forceinline__ void ln_rows_finish(const LnArgs& ln, int M, int K, float4 (&xv)[MM][4],
                                                const float (&c)[MM], const uint2 (&gb)[4][2], bf16* xs,
                                                float* scratch) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool active = threadIdx.x < 256;
   float s1[MM], s2[MM];
 #pragma unroll
   for (int m = 0; m < MM; m++) {
@@ -502,7 +517,7 @@ __device__ __forceinline__ void ln_rows_finish(const LnArgs& ln, int M, int K, f
     s1[m] = wave_sum(a1);
     s2[m] = wave_sum(a2);
   }
-  if (lane == 0) {
+  if (lane == 0 && active) {
 #pragma unroll
     for (int m = 0; m < MM; m++) {
       scratch[w * 8 + m] = s1[m];
@@ -522,7 +537,7 @@ __device__ __forceinline__ void ln_rows_finish(const LnArgs& ln, int M, int K, f
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const int k = threadIdx.x * 4 + i * 1024;
-    if (k < K) {
+    if (k < K && active) {
       const uint2 graw = gb[i][0], braw = gb[i][1];
       const float g[4] = {__uint_as_float(graw.x << 16), __uint_as_float(graw.x & 0xFFFF0000u),
                           __uint_as_float(graw.y << 16), __uint_as_float(graw.y & 0xFFFF0000u)};
@@ -557,6 +572,16 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(LnArgs ln, int K, bf16* __
   ln_rows_finish<1>(lr, 1, K, xv, c, gb, out + (size_t)blockIdx.x * K, scratch);
 }
 
+// Diagnostic builds only (tools/gemv_timeline.hip defines BS_STAMPS): wave 0 of every block records
+// s_memrealtime (100 MHz, chip-wide) at kernel entry, after the prologue, after the K loop and after the
+// epilogue.  The product library never defines it.
+#ifdef BS_STAMPS
+__device__ unsigned long long g_stamps[65536 * 4];
+#define BS_STAMP(i) do { if (threadIdx.x == 0) g_stamps[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define BS_STAMP(i) do {} while (0)
+#endif
+
 // Activation prologue of gemv_rows_kernel: X read as given, LayerNorm of fp32 rows, or the merge
 // of split-attention partials (attn_merge.h); the last two stage bf16 rows in LDS.
 enum XMode : int { X_PLAIN = 0, X_LN = 1, X_PARTS = 2 };
@@ -564,15 +589,18 @@ constexpr int kPartsPre = 2;  // 4-column groups per thread whose partial loads 
 
 // FL: probe flags for tools/gemv_probe.hip (0 in the product): 1 = temporal (not non-temporal) weight loads,
 // 2 = no activation loads (x = 1), 4 = no epilogue (a store that never fires keeps the math).
-template <int R, int MM, int U, int XM, int FL = 0>
-__global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
-                                                        LnArgs ln, AttnParts pa, int M, int N, int K, Epi ep) {
+// Block = blockDim.x / 64 waves (1..16): the dispatch sizes blocks so the grid is ~one block per CU
+// and every CU streams the same number of weight bytes (gemv_rows_dispatch).
+template <int R, int MM, int U, int XM, int FL = 0, int LB = 256>  // LB: threads the registers are bounded for
+__global__ __launch_bounds__(LB) void gemv_rows_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
+                                                         LnArgs ln, AttnParts pa, int M, int N, int K, Epi ep) {
   constexpr bool LN = XM == X_LN;
+  BS_STAMP(0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* scratch = reinterpret_cast<float*>(smem);                  // 64 floats
   bf16* xs = reinterpret_cast<bf16*>(smem + 256);                    // LN / PARTS: [M][K]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int n0 = (blockIdx.x * 4 + w) * R;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int n0 = (blockIdx.x * nw + w) * R;
   const bf16* wr[R];
 #pragma unroll
   for (int r = 0; r < R; r++) wr[r] = W + (size_t)min(n0 + r, N - 1) * K;
@@ -585,7 +613,9 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
   float4 xv[LN ? MM : 1][4];
   float xc[LN ? MM : 1];
   uint2 gb[4][2];
-  if constexpr (LN) ln_rows_load<MM>(ln, M, K, xv, xc, gb);
+  if constexpr (LN) {
+    if (threadIdx.x < 256) ln_rows_load<MM>(ln, M, K, xv, xc, gb);
+  }
   const int kq = K >> 2, ngroups = M * kq;  // PARTS: 4-column groups of all rows
   PartsRegs pr[XM == X_PARTS ? kPartsPre : 1];
   auto pld1 = [](const float* p, size_t i) { return p[i]; };
@@ -593,7 +623,7 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
   if constexpr (XM == X_PARTS) {
 #pragma unroll
     for (int it = 0; it < kPartsPre; it++) {
-      const int g = min((int)threadIdx.x + it * 256, ngroups - 1);
+      const int g = min((int)threadIdx.x + it * (int)blockDim.x, ngroups - 1);
       attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, pr[it]);
     }
   }
@@ -621,10 +651,10 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
     };
 #pragma unroll
     for (int it = 0; it < kPartsPre; it++) {
-      const int g = threadIdx.x + it * 256;
+      const int g = threadIdx.x + it * blockDim.x;
       if (g < ngroups) put(g, pr[it]);
     }
-    for (int g = threadIdx.x + kPartsPre * 256; g < ngroups; g += 256) {  // wide rows: load as we go
+    for (int g = threadIdx.x + kPartsPre * blockDim.x; g < ngroups; g += blockDim.x) {  // wide rows: load as we go
       PartsRegs r;
       attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, r);
       put(g, r);
@@ -634,6 +664,7 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
   } else {
     xg = X; xstride = K;
   }
+  BS_STAMP(1);
   float acc[R][MM];
 #pragma unroll
   for (int r = 0; r < R; r++)
@@ -665,6 +696,7 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
       }
     }
   }
+  BS_STAMP(2);
 #pragma unroll
   for (int r = 0; r < R; r++)
 #pragma unroll
@@ -705,6 +737,7 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16* __restrict__
       }
     }
   });
+  BS_STAMP(3);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1189,10 +1222,34 @@ static int gemv_waves(int N, int K) {
 
 template <int R, int MM, int XM, int U = 2, int FL = 0>
 static void gemv_rows_launch(const bf16* X, const LnArgs& ln, const AttnParts& pa, const bf16* W, int M, int N,
-                             int K, const Epi& ep, hipStream_t s) {
+                             int K, const Epi& ep, hipStream_t s, int waves = 4) {
   const size_t shm = 256 + (XM != X_PLAIN ? (size_t)M * K * sizeof(bf16) : 0);
-  const int blocks = (N + 4 * R - 1) / (4 * R);
-  gemv_rows_kernel<R, MM, U, XM, FL><<<blocks, 256, shm, s>>>(W, X, ln, pa, M, N, K, ep);
+  const int blocks = (N + waves * R - 1) / (waves * R);
+  if (waves <= 4) {
+    gemv_rows_kernel<R, MM, U, XM, FL, 256><<<blocks, waves * 64, shm, s>>>(W, X, ln, pa, M, N, K, ep);
+  } else if constexpr (MM <= 2) {  // wide blocks: <= 128 VGPRs (rows_geometry keeps R x U small)
+    gemv_rows_kernel<R, MM, U, XM, FL, 1024><<<blocks, waves * 64, shm, s>>>(W, X, ln, pa, M, N, K, ep);
+  }
+}
+
+// Rows GEMV geometry: every CU streams the same number of weight bytes.  A CU pulls ~24 GB/s of a
+// chip-wide stream (MI355X_MICROARCH.md: ~10 B/cycle/CU), so a grid of 4-wave blocks that puts 3 blocks
+// on some CUs and 2 on others (bloom-1b1 QKV: 576 blocks) ends when the 3-block CUs do: the in-kernel
+// timeline (tools/gemv_timeline.hip) showed 2 us between the first and last block's end.  Here a block
+// holds ceil(N / 256) rows (R per wave, <= 16 waves), so the grid is ~256 equal blocks.
+static bool rows_per_cu_enabled() {  // BS_ROWS_CU=0: the old fixed 4-wave blocks (A/B switch)
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("BS_ROWS_CU"); v = (e && *e == '0') ? 0 : 1; }
+  return v == 1;
+}
+static void rows_geometry(int N, int K, int M, int r_default, int* R, int* waves) {
+  if (!rows_per_cu_enabled() || M > 2) { *R = r_default; *waves = 4; return; }
+  const int rows_cu = (N + 255) / 256;
+  int r = K <= 2048 ? 2 : 1;
+  while ((rows_cu + r - 1) / r > 16 && r < 4) r *= 2;
+  if ((rows_cu + r - 1) / r < 4) r = 1;  // the LayerNorm / merge prologues need >= 4 waves (256 threads)
+  *R = r;
+  *waves = std::max(4, std::min(16, (rows_cu + r - 1) / r));
 }
 
 template <int XM>
@@ -1225,18 +1282,27 @@ static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const AttnParts&
   // LN-fused: >= 2 rows per wave halves the blocks that each redo the row's LayerNorm
   // (profiles/r01_ln_rows_sweep.txt: 560m 1566 -> 1621 tok/s, 1b1 1229 -> 1242)
   static const int plain_r = [] { const char* e = getenv("BS_PLAIN_R"); return e && *e ? atoi(e) : 0; }();  // sweeps
-  const int R = !LN ? (plain_r ? plain_r : (K <= 2048 ? 2 : 1)) : (N >= 12288 ? 4 : (N >= 2048 ? 2 : 1));
+  const int R0 = !LN ? (plain_r ? plain_r : (K <= 2048 ? 2 : 1)) : (N >= 12288 ? 4 : (N >= 2048 ? 2 : 1));
+  int R, waves;
+  rows_geometry(N, K, M, R0, &R, &waves);
   // U = 512-element chunks of a row in flight per iteration: an exact divisor of the row's chunk
   // count, so every row streams in whole rounds with no re-loaded tail (K = 1536 -> 3, 6144 -> 12,
   // 4096 -> 8, 16384 -> 8, 2560 -> 5, 1024 -> 2); fallback 4.
   const int cpr = K / 512;
-  const int U = (K % 512) ? 4 : (cpr <= 3 || cpr == 5 || cpr == 8 || cpr == 12) ? cpr
-              : (cpr % 12 == 0 ? 12 : (cpr % 8 == 0 ? 8 : (cpr % 5 == 0 ? 5 : 4)));
+  int U = (K % 512) ? 4 : (cpr <= 3 || cpr == 5 || cpr == 8 || cpr == 12) ? cpr
+        : (cpr % 12 == 0 ? 12 : (cpr % 8 == 0 ? 8 : (cpr % 5 == 0 ? 5 : 4)));
+  // wide blocks are bounded for 1024 threads (<= 128 VGPRs): keep the weight registers (R x U x 4 VGPRs)
+  // small enough that nothing spills (LayerNorm / merge prologues hold ~32 more); 8 KB per wave x up
+  // to 16 waves per CU is plenty in flight
+  if (waves > 4) {
+    const int cap = (XM == X_PLAIN ? 12 : 8) / (M == 1 ? 1 : 2);  // measured spill-free (ISA metadata)
+    while (R * U > cap) U = (U % 2 == 0) ? U / 2 : (U > 4 ? 4 : U - 1);
+  }
   auto go = [&](auto rc, auto uc) {
     constexpr int RR = decltype(rc)::value, UU = decltype(uc)::value;
-    if (M == 1) gemv_rows_launch<RR, 1, XM, UU>(x, ln, pa, w, M, N, K, ep, s);
-    else if (M == 2) gemv_rows_launch<RR, 2, XM, UU>(x, ln, pa, w, M, N, K, ep, s);
-    else gemv_rows_launch<RR, 4, XM, UU>(x, ln, pa, w, M, N, K, ep, s);
+    if (M == 1) gemv_rows_launch<RR, 1, XM, UU>(x, ln, pa, w, M, N, K, ep, s, waves);
+    else if (M == 2) gemv_rows_launch<RR, 2, XM, UU>(x, ln, pa, w, M, N, K, ep, s, waves);
+    else gemv_rows_launch<RR, 4, XM, UU>(x, ln, pa, w, M, N, K, ep, s, waves);
   };
   auto gu = [&](auto rc) {
     switch (U) {
