@@ -325,7 +325,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or args.gpus > 1:
         from distributed_inference_demo_amd.pipeline import bench_pipeline
-        res = bench_pipeline(args)
+        res, ranges, model = bench_pipeline(args)
+        if res is not None and args.cpu_baseline:  # rank 0, after the process group is gone
+            res["cpu_baseline"] = cpu_baseline(model, args.cpu_steps, args.seed, ranges=ranges)
     else:
         res = bench_single(args)
     if res is not None:

@@ -1584,10 +1584,10 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   if (threadIdx.x < hd) {
     float mx = -INFINITY;
     float acc2 = 0.f, lsum = 0.f;
-    for (int t0 = 0; t0 < nsplit; t0 += 8) {
-      float m8[8], l8[8], o8[8];
+    for (int t0 = 0; t0 < nsplit; t0 += 16) {
+      float m8[16], l8[16], o8[16];  // all of a group's loads in flight together
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < 16; u++) {
         const int t = min(t0 + u, nsplit - 1);
         m8[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(attn_rsrc(pml_g), (uint32_t)t * 8, 0, 16));
         l8[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(attn_rsrc(pml_g), (uint32_t)t * 8 + 4, 0, 16));
@@ -1596,14 +1596,14 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
       // online merge of this group of 8 (duplicates past nsplit masked out)
       float gm = -INFINITY;
 #pragma unroll
-      for (int u = 0; u < 8; u++) gm = t0 + u < nsplit ? fmaxf(gm, m8[u]) : gm;
+      for (int u = 0; u < 16; u++) gm = t0 + u < nsplit ? fmaxf(gm, m8[u]) : gm;
       const float nm = fmaxf(mx, gm);
       if (nm != -INFINITY) {
         const float sc = __expf(mx - nm);  // mx = -inf on the first group: 0
         acc2 *= sc;
         lsum *= sc;
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < 16; u++) {
           if (t0 + u < nsplit && m8[u] != -INFINITY) {
             const float wgt = __expf(m8[u] - nm);
             acc2 += wgt * o8[u];
@@ -1880,11 +1880,25 @@ size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, 
 // otherwise 4-wave blocks split the context so ~256 blocks stream the KV cache (>= one 64-position
 // chunk per wave at full cache).  Static per (B, n_head, cache size), so the consumer of a deferred
 // merge knows it without a device round trip.
+// Wide decode attention (few (row, head) pairs): 2-wave blocks of 32-position chunks, one block per 64
+// cached positions, so the KV stream spreads over ~all CUs (a CU pulls ~24 GB/s of a chip-wide stream:
+// 48 blocks for bloom-1b1 B = 1 left 70 KB of K/V per CU, ~3 us); the last split block of each
+// (row, head) merges by ticket and writes ctx, so the dense GEMV after it needs no merge prologue.
+// Measured (profiles/r02_attn_wide_ab.txt): bloom-7b1 B = 1 ctx ~200 +1.7 %, bloom-1b1 B = 1 ctx ~600 -4 %
+// (the ticket merge's atomic + reload round trips on the last block cost more than the narrow kernel's
+// per-CU stream); off by default, BS_ATTN_WIDE=1 turns it on.
+static bool attn_wide() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("BS_ATTN_WIDE"); v = (e && *e == '1') ? 1 : 0; }
+  return v == 1;
+}
+
 int attention_decode_splits(int B, int n_head, int max_chunks) {
   static const int forced = [] { const char* e = getenv("BS_ATTN_SPLITS"); return e && *e ? atoi(e) : 0; }();  // sweeps
   if (forced > 0) return min(forced, max(1, max_chunks));
   const int pairs = B * n_head;
   if (pairs >= 192 || max_chunks <= 4) return 1;
+  if (attn_wide()) return max(1, min(max_chunks, 512 / pairs));
   const int nsplit = min((256 + pairs - 1) / pairs, (max_chunks + 3) / 4);
   return max(1, min(nsplit, 64));
 }
@@ -1904,6 +1918,9 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
       dim3 g(a.n_head, a.B, 1);
       if (is_bf16) attn_decode_kernel<bf16, 8><<<g, 512, 0, s>>>(a);
       else attn_decode_kernel<float, 8><<<g, 512, 0, s>>>(a);
+    } else if (is_bf16 && !a.defer_merge && attn_wide()) {
+      dim3 g(a.n_head, a.B, nsplit);
+      attn_decode_kernel<bf16, 2, 32><<<g, 128, 0, s>>>(a);
     } else if (is_bf16 && a.defer_merge && attn_small_chunks()) {
       // few (row, head) pairs: 8 waves x 32 positions per block, half the serial work per wave
       dim3 g(a.n_head, a.B, nsplit);

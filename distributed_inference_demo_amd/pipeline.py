@@ -88,6 +88,7 @@ class Pipeline:
         self.pending = [[] for _ in range(n_mb)]
         self.hpending = [[] for _ in range(n_mb)]
         self.past = [0] * n_mb
+        self.tokens_held = False  # after finish(): rank 0 already holds every micro-batch's next input
         if self.head_split:
             self.xn = [torch.empty(mb_rows * hidden, dtype=act_dtype, device=device) for _ in range(n_mb)]
             self.kin = [torch.zeros(mb_rows, dtype=torch.int64, device=device) for _ in range(n_mb)]
@@ -151,7 +152,8 @@ class Pipeline:
                 if prompt is not None:
                     inp = prompt[j * self.mb:(j + 1) * self.mb].contiguous()
                 else:
-                    self._token_in(j, record)
+                    if not self.tokens_held:
+                        self._token_in(j, record)
                     inp = self.tok[j]
             else:
                 inp = self.hin[j][:n_el]
@@ -175,12 +177,15 @@ class Pipeline:
             if self.head_split and self.rank <= self.closer:
                 self._head_role(j, record)
             self.past[j] += seq
+        self.tokens_held = False
 
     def finish(self, record=None):
-        """Rank 0 collects the tokens of the last round; everyone drains its sends."""
-        if self.is_first and self.world > 1:
+        """Rank 0 collects the tokens of the last round; everyone drains its sends.  Later steps
+        continue from those tokens."""
+        if self.is_first and self.world > 1 and not self.tokens_held:
             for j in range(self.n_mb):
                 self._token_in(j, record)
+            self.tokens_held = True
         for j in range(self.n_mb):
             self._drain(self.pending[j])
             self._drain(self.hpending[j])
@@ -264,17 +269,29 @@ def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb
     return pipe, (lb, le)
 
 
+def _stage_step_bytes(model, lb, le, rows, ctx, first, last, hslice, w_bytes, kv_bytes):
+    """Algorithmic HBM bytes of one decode forward of a stage (BASELINE.md formula) plus, with the
+    vocabulary-parallel head, the stage's lm_head slice and ln_f."""
+    b = config.decode_step_bytes(model, le - lb, rows, ctx, first, last, w_bytes=w_bytes, kv_bytes=kv_bytes)
+    if hslice is not None:
+        b += (hslice[1] - hslice[0]) * model.hidden * w_bytes + 2 * model.hidden * w_bytes
+    return b
+
+
 def bench_pipeline(args):
-    """bench.py --gpus N under torchrun: N stages, N micro-batches of `batch` rows in flight."""
+    """bench.py --gpus N under torchrun: N stages, n_mb micro-batches of `batch` rows in flight.
+    Rank 0 returns the JSON dict (with per-stage roofline / HBM figures gathered from every rank) and
+    the stage ranges (for the host-CPU baseline of the same split)."""
     rank, world, local = init_distributed("nccl")
     dev = torch.device("cuda", local)
     model = config.get(args.model)
     if getattr(args, "weights", "bf16") == "int8":
         model = config.get(model.name if model.int8_weights else model.name + "-int8")
     B, P, K, W = args.batch, args.prompt, args.steps, args.warmup
+    prof_rounds = 0 if getattr(args, "no_profile", False) else 8
     head_split = not getattr(args, "no_head_split", False)
-    pipe, (lb, le) = build_rank(model, rank, world, dev, dtype=args.dtype, mb_rows=B, max_ctx=P + W + K + 2,
-                                max_seq=P, seed=args.seed, head_split=head_split)
+    pipe, (lb, le) = build_rank(model, rank, world, dev, dtype=args.dtype, mb_rows=B,
+                                max_ctx=P + W + K + prof_rounds + 2, max_seq=P, seed=args.seed, head_split=head_split)
     n_mb = pipe.n_mb
     cs = torch.cuda.Stream()  # a real stream: decode steps are captured as hipGraphs
     torch.cuda.set_stream(cs)
@@ -302,10 +319,40 @@ def bench_pipeline(args):
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
+    t_round = dt / K
+    # per-stage roofline: eager rounds with HIP events around every decode weight GEMV of this stage
+    st = pipe.ex.stage if hasattr(pipe.ex, "stage") else None
+    g = None
+    if st is not None and prof_rounds:
+        st.profile_enable(1)
+        for _ in range(prof_rounds):
+            pipe.step(1)
+        pipe.finish()
+        torch.cuda.synchronize()
+        g = st.profile_read()
+        st.profile_enable(0)
+    dist.barrier()
+    hslice = vocab_slices(model.vocab, world)[rank] if pipe.head_split else None
+    w_b = 2 if args.dtype == "bf16" else 4
+    ctx_mid = P + W + K / 2
+    step_bytes = _stage_step_bytes(model, lb, le, B, ctx_mid, rank == 0, rank == world - 1 and not pipe.head_split,
+                                   hslice, w_b, w_b)
+    if model.int8_weights:
+        step_bytes -= (le - lb) * (12.0 * model.hidden * model.hidden * 1 - 9.0 * model.hidden * 4)
+    mine = {"rank": rank, "layers": [lb, le], "head_slice": list(hslice) if hslice else None,
+            "algo_bytes_per_forward": step_bytes,
+            "achieved_GBps": n_mb * step_bytes / t_round / 1e9}
+    mine["frac_of_peak"] = mine["achieved_GBps"] / 8000.0
+    if g is not None and g[1]:
+        ms, n, byts = g
+        mine["gemv"] = {"launches": n, "avg_us": ms / n * 1e3, "achieved_GBps": (byts / n) / (ms / n * 1e-3) / 1e9}
+    allst = [None] * world
+    dist.all_gather_object(allst, mine)
     per_stage = [b - a for a, b in stage_ranges(world, model.n_layer)]
     res = None
     if rank == 0:
         toks = B * n_mb * K
+        gemv = [x["gemv"] for x in allst if "gemv" in x]
         res = {
             "metric": "decode tokens/s, BLOOM pipeline", "value": toks / dt, "unit": "tokens/s", "n_gpus": world,
             "steps": K, "warmup": W, "ms_per_step": dt * 1e3 / K, "higher_is_better": True, "scaling": "weak",
@@ -316,9 +363,25 @@ def bench_pipeline(args):
                                    + (", vocabulary-parallel lm_head ring" if pipe.head_split else ""),
                        "model": model.name, "stages": world, "layers_per_stage": per_stage, "batch": B * n_mb,
                        "micro_batch": B, "prompt": P, "parallelism": f"pp{world}",
-                       "head": "vocab-split ring" if pipe.head_split else "last stage"},
+                       "head": "vocab-split ring" if pipe.head_split else "last stage",
+                       "hop": "fp32 hidden [mb, S, h] (the reference wire dtype; keeps the split bit-identical to one stage)"},
             "prefill_plus_warmup_s": t_prefill_warm,
+            "per_stage": allst,
+            "stage_hbm": {"achieved_GBps_min": min(x["achieved_GBps"] for x in allst),
+                          "achieved_GBps_mean": sum(x["achieved_GBps"] for x in allst) / world,
+                          "frac_of_peak_min": min(x["frac_of_peak"] for x in allst),
+                          "frac_of_peak_mean": sum(x["frac_of_peak"] for x in allst) / world,
+                          "note": "per stage: n_mb x algorithmic bytes of one forward / time of one pipeline round"},
         }
+        if gemv:
+            tot_t = sum(x["launches"] * x["avg_us"] for x in gemv)
+            tot_b = sum(x["launches"] * x["avg_us"] * 1e-6 * x["achieved_GBps"] * 1e9 for x in gemv)
+            ach = tot_b / (tot_t * 1e-6) / 1e9
+            res["roofline"] = {"bound": "hbm", "kernel": "gemv_rows_kernel (decode weight GEMVs of every stage)",
+                               "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0, "traffic": None,
+                               "launches": sum(x["launches"] for x in gemv), "avg_us": tot_t / sum(x["launches"] for x in gemv),
+                               "measured": f"HIP events per launch on each stage's stream, {prof_rounds} eager pipeline "
+                                           "rounds after the timed region; bytes and time summed over all stages"}
     dist.barrier()
     dist.destroy_process_group()
-    return res
+    return res, stage_ranges(world, model.n_layer), model

@@ -45,14 +45,21 @@ class OracleExecutor:
         out.copy_(torch.from_numpy(np.ascontiguousarray(y).reshape(-1)[: out.numel()]).view(out.shape))
 
 
-def _worker(rank, world, port, q, head_split=False):
+def _worker(rank, world, port, q, head_split=False, resume=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        pipe, _ = build_rank(MODEL, rank, world, torch.device("cpu"), mb_rows=MB, max_ctx=P + STEPS + 2,
+        pipe, _ = build_rank(MODEL, rank, world, torch.device("cpu"), mb_rows=MB, max_ctx=P + STEPS + resume + 2,
                              max_seq=P, executor_factory=OracleExecutor, head_split=head_split, dtype="fp32")
         prompt = torch.from_numpy(prompt_ids(1234, MB * pipe.n_mb, P, MODEL.vocab)) if rank == 0 else None
         toks = generate(pipe, prompt, STEPS, P)
+        if resume:  # rounds after finish() continue from the tokens finish() collected
+            rec = [[] for _ in range(pipe.n_mb)] if rank == 0 else None
+            for _ in range(resume):
+                pipe.step(1, record=rec)
+            pipe.finish(record=rec)
+            if rank == 0:
+                toks = torch.cat([toks, torch.cat([torch.stack(r, 1) for r in rec], 0)], 1)
         if rank == 0:
             q.put(toks.numpy())
         dist.barrier()
@@ -68,12 +75,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,head_split", [(2, False), (3, False), (2, True), (3, True), (4, True)])
-def test_pipeline_matches_single_stage(world, head_split):
+@pytest.mark.parametrize("world,head_split,resume", [(2, False, 0), (3, False, 0), (2, True, 0), (3, True, 0),
+                                                     (4, True, 0), (2, False, 3), (3, True, 3)])
+def test_pipeline_matches_single_stage(world, head_split, resume):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, head_split)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, head_split, resume)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
@@ -84,10 +92,10 @@ def test_pipeline_matches_single_stage(world, head_split):
     B = got.shape[0]
     assert B == MB * world * (2 if head_split else 1)
     ref = OracleStage(MODEL.hidden, MODEL.n_head, MODEL.n_layer, MODEL.vocab, 0, MODEL.n_layer, max_batch=B,
-                      max_ctx=P + STEPS + 2, seed=SEED)
+                      max_ctx=P + STEPS + resume + 2, seed=SEED)
     tok = ref.forward(prompt_ids(1234, B, P, MODEL.vocab), B, P)
     want = [tok]
-    for i in range(STEPS):
+    for i in range(STEPS + resume):
         tok = ref.forward(tok.reshape(B, 1), B, 1, past_len=P + i)
         want.append(tok)
     assert np.array_equal(got, np.stack(want, 1))
