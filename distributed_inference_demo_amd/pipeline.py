@@ -140,13 +140,19 @@ class Pipeline:
         if record is not None:
             record[j].append(self.tok[j].clone())
 
-    def step(self, seq, prompt=None, record=None):
+    def step(self, seq, prompt=None, record=None, feed=None, pasts=None):
         """One pipeline round: every micro-batch advances by `seq` tokens (seq = prompt length
         on the prefill round, 1 on decode rounds).  `prompt` [n_mb*mb, seq] int32 on rank 0
-        for the prefill round; rank 0 appends the tokens it receives to `record`."""
+        for the prefill round; rank 0 appends the tokens it receives to `record`.
+        Continuous batching (serve.py): `pasts[j]` = every row's own position this round (all
+        ranks, the same schedule); `feed[j]` = (tokens, mask) int32/bool [mb] on rank 0's device:
+        rows with mask set take `tokens` (a prompt token, or a new sample's first token) instead of
+        the token the pipeline returned for them."""
         n_el = self.mb * seq * self.h
         for j in range(self.n_mb):
             slot = j * self.mb
+            if pasts is not None:
+                self.past[j] = list(pasts[j])
             self._drain(self.pending[j])
             if self.is_first:
                 if prompt is not None:
@@ -155,6 +161,8 @@ class Pipeline:
                     if not self.tokens_held:
                         self._token_in(j, record)
                     inp = self.tok[j]
+                    if feed is not None:
+                        inp = torch.where(feed[j][1], feed[j][0], inp)
             else:
                 inp = self.hin[j][:n_el]
                 _recv(inp, self.rank - 1)
@@ -176,7 +184,7 @@ class Pipeline:
                     self.pending[j].append(dist.isend(self.kout[j], dst=0, group=self.head_group))
             if self.head_split and self.rank <= self.closer:
                 self._head_role(j, record)
-            self.past[j] += seq
+            self.past[j] = [p + seq for p in self.past[j]] if isinstance(self.past[j], list) else self.past[j] + seq
         self.tokens_held = False
 
     def finish(self, record=None):

@@ -10,11 +10,15 @@ num_device, graph, ...}, places contiguous layer ranges with `round_robin_module
 Here: one process per GPU (torchrun), rank r = device r of the graph, layers from the same
 placement (`placement.stage_ranges`).  Lifecycle:
   init   — RunConfig -> this rank's stage + Pipeline (`pipeline.build_rank`); the `core_pool_size`
-           samples in flight = min(pool, stages) micro-batches x the rest as rows (each sample
-           owns a KV slot), so every stage computes while the hops overlap;
-  run    — samples in waves of the pool: one prompt prefill round, then max_length - 1
-           decode rounds, all micro-batches in flight through the stages (a short last wave is
-           padded with copies of its last sample, whose outputs are dropped);
+           samples in flight = min(pool, stages) micro-batches x the rest as rows, every row a KV slot
+           holding one sample at its own position (bs_step.past_lens), so every stage computes while
+           the hops overlap;
+  run    — continuous admission (Communication.java:418-464: a new sample starts as soon as one in
+           flight finishes): a row takes the next sample the round its previous sample produced its
+           `max_length`-th token.  Rounds are S = 1 for every row: a sample's prompt is fed one token
+           a round (the reference header also feeds single tokens, Communication.java:322-326), then
+           its own greedy tokens.  Prompts may have different lengths.  The admission schedule depends
+           only on the prompt lengths, so every rank derives the same per-row positions;
   finish — rank 0 returns every sample's `max_length` greedy token ids and the run's tokens/s.
 Differences from the reference, by design: full-context decode (the reference
 header feeds only the last token), argmax instead of unseeded top-k, token ids in (no tokenizer).
@@ -57,10 +61,26 @@ def synthetic_prompts(cfg: RunConfig, vocab):
     return [prompt_ids(1234 + i, 1, cfg.prompt_len, vocab).reshape(-1).tolist() for i in range(cfg.num_sample)]
 
 
+def admission_schedule(lens, max_length, rows):
+    """Row-level continuous admission: sample i (in order) takes the row that frees first (lowest row
+    on ties) at the round it frees; it occupies the row for len(prompt) - 1 + max_length rounds (its
+    prompt tokens, then max_length generated ones, the last of which is never fed back).
+    Returns ([(row, start_round)] per sample, total rounds)."""
+    import heapq
+    free = [(0, r) for r in range(rows)]
+    heapq.heapify(free)
+    out = []
+    for n in lens:
+        t, r = heapq.heappop(free)
+        out.append((r, t))
+        heapq.heappush(free, (t + n - 1 + max_length, r))
+    return out, max(t + n - 1 + max_length for (r, t), n in zip(out, lens))
+
+
 def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory=None, log=None):
-    """Run the whole job on this rank.  `prompts` (rank 0): num_sample lists of token ids, all of
-    one length (None: synthetic).  Returns {"samples": [[max_length ids] per sample], ...} on
-    rank 0, None elsewhere.  Collective: every rank calls it with the same cfg."""
+    """Run the whole job on this rank.  `prompts` (rank 0): num_sample lists of token ids of any
+    lengths (None: synthetic).  Returns {"samples": [[max_length ids] per sample], ...} on rank 0,
+    None elsewhere.  Collective: every rank calls it with the same cfg."""
     say = log if (log is not None and rank == 0) else (lambda *_: None)
     if cfg.num_sample < 1 or cfg.max_length < 1 or cfg.core_pool_size < 1:
         raise ValueError("num_sample, max_length and core_pool_size must be >= 1")
@@ -69,53 +89,57 @@ def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory
         prompts = synthetic_prompts(cfg, model.vocab) if prompts is None else [list(p) for p in prompts]
         if len(prompts) != cfg.num_sample:
             raise ValueError(f"{len(prompts)} prompts for num_sample = {cfg.num_sample}")
-        lens = {len(p) for p in prompts}
-        if len(lens) != 1:
-            raise ValueError("all prompts of a run must have one length (no padding masks on this path)")
-        plen = lens.pop()
+        if any(len(p) < 1 for p in prompts):
+            raise ValueError("every prompt needs at least one token")
+        lens = [len(p) for p in prompts]
     else:
-        plen = cfg.prompt_len
-    if world > 1:  # the prompt length travels with the config (server -> devices)
-        t = torch.tensor([plen], dtype=torch.int64)
+        lens = [0] * cfg.num_sample
+    if world > 1:  # the prompt lengths travel with the config (server -> devices)
+        t = torch.tensor(lens, dtype=torch.int64)
         if dist.get_backend() == "nccl":
             t = t.to(device)
         dist.broadcast(t, src=0)
-        plen = int(t.item())
+        lens = [int(v) for v in t.tolist()]
     # samples in flight = n_mb micro-batches x mb rows: one micro-batch per stage keeps every stage
     # busy; the rest of the pool rides as rows of a micro-batch (one GPU: one batched decode)
     n_mb = min(cfg.core_pool_size, world)
     mb = -(-cfg.core_pool_size // n_mb)
-    pool = n_mb * mb
+    rows = n_mb * mb
+    sched, T = admission_schedule(lens, cfg.max_length, rows)
+    # per round and row: position, and (rank 0) the fed token / whether it overrides the returned one
+    pos = [[0] * rows for _ in range(T)]
+    feed_tok = [[0] * rows for _ in range(T)]
+    feed_mask = [[True] * rows for _ in range(T)]
+    for i, ((r, t0), n) in enumerate(zip(sched, lens)):
+        for t in range(t0, t0 + n - 1 + cfg.max_length):
+            pos[t][r] = t - t0
+            if t - t0 < n:
+                feed_tok[t][r] = prompts[i][t - t0] if rank == 0 else 0
+            else:
+                feed_mask[t][r] = False
     # ---- init (Ready)
     pipe, (lb, le) = build_rank(model, rank, world, device, dtype=cfg.dtype, mb_rows=mb, n_mb=n_mb,
-                                max_ctx=plen + cfg.max_length + 1, max_seq=plen, seed=cfg.seed,
+                                max_ctx=max(lens) + cfg.max_length + 1, max_seq=1, seed=cfg.seed,
                                 head_split=cfg.head_split, executor_factory=executor_factory)
     say(STATES[0], {"rank_layers": [lb, le], "stages": world, "core_pool_size": cfg.core_pool_size,
-                    "micro_batches": n_mb, "rows_per_micro_batch": mb})
+                    "micro_batches": n_mb, "rows_per_micro_batch": mb, "rounds": T})
     cuda = device.type == "cuda"
     if cuda:
         torch.cuda.set_stream(torch.cuda.Stream(device))  # decode steps are captured as hipGraphs
+    ft = torch.tensor(feed_tok, dtype=torch.int32, device=device).view(T, n_mb, mb)
+    fm = torch.tensor(feed_mask, dtype=torch.bool, device=device).view(T, n_mb, mb)
     if world > 1:
         dist.barrier()
     # ---- run (Running)
     say(STATES[1], {"num_sample": cfg.num_sample, "max_length": cfg.max_length})
-    out = []
+    rec = [[] for _ in range(n_mb)] if pipe.is_first else None
+    pipe.tokens_held = True  # round 0 feeds every row
     t0 = time.perf_counter()
-    for w0 in range(0, cfg.num_sample, pool):
-        prompt = None
-        if rank == 0:
-            wave = prompts[w0:w0 + pool]
-            wave = wave + [wave[-1]] * (pool - len(wave))  # pad a short last wave
-            prompt = torch.tensor(wave, dtype=torch.int32, device=device)
-        pipe.past = [0] * n_mb  # each micro-batch's slot starts a new sample
-        rec = [[] for _ in range(n_mb)] if pipe.is_first else None
-        pipe.step(plen, prompt=prompt, record=rec)
-        for _ in range(cfg.max_length - 1):
-            pipe.step(1, record=rec)
-        pipe.finish(record=rec)
-        if rank == 0:
-            ids = torch.cat([torch.stack(r, 1) for r in rec], 0).cpu()
-            out.extend(ids[: min(pool, cfg.num_sample - w0)].tolist())
+    for t in range(T):
+        pasts = [pos[t][j * mb:(j + 1) * mb] for j in range(n_mb)]
+        feed = [(ft[t, j], fm[t, j]) for j in range(n_mb)] if pipe.is_first else None
+        pipe.step(1, record=rec, feed=feed, pasts=pasts)
+    pipe.finish(record=rec)
     if cuda:
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -124,9 +148,11 @@ def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory
         dist.barrier()
     if rank != 0:
         return None
+    y = torch.stack([torch.stack(r, 0) for r in rec], 1).view(T, rows).cpu()  # returned token of round t
+    out = [y[t0 + n - 1:t0 + n - 1 + cfg.max_length, r].tolist() for (r, t0), n in zip(sched, lens)]
     res = {"samples": out, "num_sample": cfg.num_sample, "max_length": cfg.max_length,
-           "core_pool_size": cfg.core_pool_size, "stages": world, "prompt_len": plen, "seconds": dt,
-           "tokens_per_s": cfg.num_sample * cfg.max_length / dt}
+           "core_pool_size": cfg.core_pool_size, "stages": world, "prompt_lens": lens, "rounds": T,
+           "seconds": dt, "tokens_per_s": cfg.num_sample * cfg.max_length / dt}
     say(STATES[2], {k: v for k, v in res.items() if k != "samples"})
     say(STATES[3], {})
     return res

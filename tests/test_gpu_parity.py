@@ -387,16 +387,23 @@ def test_small_batch_decode_from_empty_cache(B, slot, hd):
             past += 1
 
 
-def test_serve_run_on_gpu_matches_oracle_per_sample():
-    """serve.py lifecycle on one GPU (fp32 stage): 5 samples in waves of 2 in flight, each
-    sample's 8 greedy ids equal to the fp32 oracle decoding that sample alone."""
+@pytest.mark.parametrize("ragged", [False, True])
+def test_serve_run_on_gpu_matches_oracle_per_sample(ragged):
+    """serve.py lifecycle on one GPU (fp32 stage): 5 samples, 2 (or 3) rows in flight with continuous
+    admission (a row takes the next sample when its sample finishes; ragged: prompts of 2..11 tokens, so
+    rows sit at different positions in every graph-replayed step), each sample's 8 greedy ids equal to
+    the fp32 oracle decoding that sample alone."""
     import torch
     from distributed_inference_demo_amd.serve import RunConfig, run_rank, synthetic_prompts
     model = BloomDims("tinygpu", 256, 2, 4, vocab=1024)  # 2 layers, 4 heads
-    cfg = RunConfig(model=model, num_sample=5, max_length=8, core_pool_size=2, prompt_len=9, dtype="fp32", seed=11)
-    res = run_rank(cfg, 0, 1, torch.device("cuda", 0))
+    cfg = RunConfig(model=model, num_sample=5, max_length=8, core_pool_size=3 if ragged else 2, prompt_len=9,
+                    dtype="fp32", seed=11)
+    prompts = synthetic_prompts(cfg, model.vocab)
+    if ragged:
+        prompts = [p[:n] + p[:max(0, n - len(p))] for p, n in zip(prompts, (2, 11, 5, 9, 3))]
+    res = run_rank(cfg, 0, 1, torch.device("cuda", 0), prompts=prompts)
     want = []
-    for p in synthetic_prompts(cfg, model.vocab):
+    for p in prompts:
         o = OracleStage(256, 4, 2, 1024, 0, 2, bf16=False, max_batch=1, max_ctx=32, seed=11)
         tok = o.forward(np.array(p, np.int32).reshape(1, -1), 1, len(p))
         ids = [int(tok[0])]

@@ -64,10 +64,24 @@ def test_serve_single_rank_given_prompts():
     prompts = rng.integers(0, MODEL.vocab, size=(3, 4)).tolist()
     cfg = RunConfig(**{**CFG.__dict__, "num_sample": 3, "core_pool_size": 2, "max_length": 4})
     res = run_rank(cfg, 0, 1, torch.device("cpu"), prompts=prompts, executor_factory=OracleExecutor)
-    assert res["prompt_len"] == 4 and res["samples"] == _reference(prompts, 4)
+    assert res["prompt_lens"] == [4, 4, 4] and res["samples"] == _reference(prompts, 4)
 
 
-def test_serve_rejects_ragged_prompts():
+def test_serve_ragged_prompts_continuous_admission():
+    """Prompts of 1..9 tokens, 3 rows in flight: a row takes the next sample the round its sample
+    finishes, rows sit at different positions; every sample's ids equal the per-sample checker."""
+    rng = np.random.default_rng(8)
+    prompts = [rng.integers(0, MODEL.vocab, size=n).tolist() for n in (5, 1, 9, 3, 2, 7)]
+    cfg = RunConfig(**{**CFG.__dict__, "num_sample": 6, "core_pool_size": 3, "max_length": 5})
+    res = run_rank(cfg, 0, 1, torch.device("cpu"), prompts=prompts, executor_factory=OracleExecutor)
+    assert res["samples"] == _reference(prompts, 5)
+    # the admission schedule: the sample after the 1-token prompt starts on that row at round 5
+    from distributed_inference_demo_amd.serve import admission_schedule
+    sched, T = admission_schedule([5, 1, 9, 3, 2, 7], 5, 3)
+    assert sched[:4] == [(0, 0), (1, 0), (2, 0), (1, 5)] and T == res["rounds"]
+
+
+def test_serve_rejects_empty_prompts():
     with pytest.raises(ValueError):
-        run_rank(RunConfig(**{**CFG.__dict__, "num_sample": 2}), 0, 1, torch.device("cpu"), prompts=[[1, 2], [3]],
+        run_rank(RunConfig(**{**CFG.__dict__, "num_sample": 2}), 0, 1, torch.device("cpu"), prompts=[[1, 2], []],
                  executor_factory=OracleExecutor)
