@@ -8,6 +8,7 @@
 // (kernels.hip) over weights, KV cache and workspace resident in the stage GPU's HBM.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -558,6 +559,76 @@ extern "C" int bs_stream_delay(void* stream, int32_t microseconds) {
   stream_delay_kernel<<<1, 1, 0, (hipStream_t)stream>>>((long long)microseconds * 100);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(BS_ERR_DEVICE, std::string("stream delay: ") + hipGetErrorString(e));
+  return BS_OK;
+}
+
+// ---- HBM probe (bench.py "hbm_measured"): STREAM-like read and copy rates of this device.
+typedef unsigned int probe_u4 __attribute__((ext_vector_type(4)));
+// Every thread keeps 8 16-B loads in flight (a 32 KB tile per 256-thread block and step), grid-stride
+// over tiles: enough bytes in flight per CU to hide HBM latency at the full rate.
+constexpr int kProbeU = 8;
+__global__ __launch_bounds__(256) void probe_read_kernel(const probe_u4* __restrict__ p, size_t n, probe_u4* sink) {
+  probe_u4 acc = {0u, 0u, 0u, 0u};
+  const size_t tile = (size_t)blockDim.x * kProbeU;
+  for (size_t t = (size_t)blockIdx.x * tile; t + tile <= n; t += (size_t)gridDim.x * tile) {
+    probe_u4 v[kProbeU];
+#pragma unroll
+    for (int u = 0; u < kProbeU; u++) v[u] = __builtin_nontemporal_load(p + t + u * blockDim.x + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < kProbeU; u++) acc ^= v[u];
+  }
+  if ((acc.x & acc.y & acc.z & acc.w) == 0xFFFFFFFFu) sink[0] = acc;  // never in practice; keeps the loads
+}
+__global__ __launch_bounds__(256) void probe_copy_kernel(const probe_u4* __restrict__ p, probe_u4* __restrict__ q, size_t n) {
+  const size_t tile = (size_t)blockDim.x * kProbeU;
+  for (size_t t = (size_t)blockIdx.x * tile; t + tile <= n; t += (size_t)gridDim.x * tile) {
+    probe_u4 v[kProbeU];
+#pragma unroll
+    for (int u = 0; u < kProbeU; u++) v[u] = __builtin_nontemporal_load(p + t + u * blockDim.x + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < kProbeU; u++) __builtin_nontemporal_store(v[u], q + t + u * blockDim.x + threadIdx.x);
+  }
+}
+
+extern "C" int bs_hbm_probe(int32_t device, uint64_t bytes, double* read_gbps, double* copy_gbps) {
+  if (bytes < (1u << 20) || bytes % (1u << 20)) return fail(BS_ERR_INVALID, "probe bytes must be a positive multiple of 1 MiB");
+  HIP_TRY(hipSetDevice(device));
+  void *a = nullptr, *b = nullptr;
+  if (hipMalloc(&a, bytes) != hipSuccess) return fail(BS_ERR_OOM, "probe allocation failed");
+  if (hipMalloc(&b, bytes) != hipSuccess) { hipFree(a); return fail(BS_ERR_OOM, "probe allocation failed"); }
+  hipStream_t st;
+  hipEvent_t e0, e1;
+  hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipMemsetAsync(a, 1, bytes, st);
+  const size_t n = bytes / 16;
+  const unsigned grid = 256 * 8;  // 8 blocks per CU
+  float best_r = 1e30f, best_c = 1e30f;
+  for (int it = 0; it < 12; it++) {
+    hipEventRecord(e0, st);
+    probe_read_kernel<<<grid, 256, 0, st>>>((const probe_u4*)a, n, (probe_u4*)b);
+    hipEventRecord(e1, st);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (it >= 2) best_r = std::min(best_r, ms);
+    hipEventRecord(e0, st);
+    probe_copy_kernel<<<grid, 256, 0, st>>>((const probe_u4*)a, (probe_u4*)b, n);
+    hipEventRecord(e1, st);
+    hipEventSynchronize(e1);
+    hipEventElapsedTime(&ms, e0, e1);
+    if (it >= 2) best_c = std::min(best_c, ms);
+  }
+  hipError_t err = hipGetLastError();
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipStreamDestroy(st);
+  hipFree(a);
+  hipFree(b);
+  if (err != hipSuccess) return fail(BS_ERR_DEVICE, std::string("probe: ") + hipGetErrorString(err));
+  if (read_gbps) *read_gbps = (double)bytes / (best_r * 1e-3) / 1e9;
+  if (copy_gbps) *copy_gbps = 2.0 * (double)bytes / (best_c * 1e-3) / 1e9;
   return BS_OK;
 }
 

@@ -81,7 +81,7 @@ EXPORTS = [
     "bs_stage_weight_count", "bs_abi_version", "bs_profile_enable", "bs_profile_read",
     "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
     "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice", "bs_stream_delay", "bs_set_sampling",
-    "bs_build_id",
+    "bs_build_id", "bs_hbm_probe",
 ]
 
 _LIB = None
@@ -130,6 +130,7 @@ def lib():
         L.bs_head_norm.argtypes = [vp, vp, i32, i32, vp, vp]
         L.bs_head_slice.argtypes = [vp, vp, i32, vp, vp, vp, vp]
         L.bs_set_sampling.argtypes = [vp, i32, ctypes.c_float, ctypes.c_uint64]
+        L.bs_hbm_probe.argtypes = [i32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         _LIB = L
     return _LIB
 
@@ -305,6 +306,13 @@ def prompt_ids(seed, batch, seq, vocab):
     out = np.empty((batch, seq), np.int32)
     _check(lib().bs_prompt_ids(seed, batch * seq, vocab, out.ctypes.data))
     return out
+
+
+def hbm_probe(device=0, nbytes=2 << 30):
+    """STREAM-like (read GB/s, copy GB/s) of a device (bs_hbm_probe)."""
+    r, c = ctypes.c_double(), ctypes.c_double()
+    _check(lib().bs_hbm_probe(device, nbytes, ctypes.byref(r), ctypes.byref(c)))
+    return r.value, c.value
 
 
 def weight_count(**kw):

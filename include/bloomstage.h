@@ -188,6 +188,10 @@ int bs_profile_read(bs_stage *stage, double *total_ms, uint64_t *launches, doubl
  * so event-timed launches are not stretched by host submission gaps. */
 int bs_stream_delay(void *stream, int32_t microseconds);
 
+/* Measurement aid (bench.py "hbm_measured"): STREAM-like HBM rates of a device, best of 10 runs over
+ * `bytes` (a multiple of 1 MiB) -- read: non-temporal 16-B loads; copy: read + write bytes / time. */
+int bs_hbm_probe(int32_t device, uint64_t bytes, double *read_gbps, double *copy_gbps);
+
 /* ---- Reference wire codec (utils.cpp:124-368): size_t n; per tensor {int32 dtype,
  * size_t ndim, int64 dims[ndim], raw little-endian data}. size_t is 8 bytes (LP64). ---- */
 #define BS_CODEC_MAX_DIMS 8
