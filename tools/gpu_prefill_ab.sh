@@ -1,8 +1,12 @@
-# prefill changes: GPU tests, bench, narrow-tile A/B, kernel stats
+# prefill GEMM A/B on the bench's prefill numbers: bash tools/gpu_prefill_ab.sh NAME "ENV_A" "ENV_B" [bench args]
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u bench.py --cpu-baseline 0 --no-pmc > gpurun_out/bench_new.log 2>&1 || exit $?
-BS_GEMM_NO_NARROW=1 timeout -k 10 300 python -u bench.py --cpu-baseline 0 --no-pmc > gpurun_out/bench_nonarrow.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o run --output-format csv -- python -u bench.py --cpu-baseline 0 --no-pmc --steps 32 > gpurun_out/prof1.log 2>&1
+name=$1; a=$2; b=$3; shift 3
+out=gpurun_out/pab_$name.log; : > $out
+for i in 1 2; do
+  for arm in "$a" "$b"; do
+    r=$(env $arm timeout -k 10 300 python -u bench.py --cpu-baseline 0 --no-pmc --steps 16 --warmup 2 "$@" 2>/dev/null | tail -1) || exit 1
+    v=$(echo "$r" | python -c 'import json,sys; d=json.loads(sys.stdin.read())["prefill"]; print("prefill %.3f ms  gemm %.1f TFLOP/s (%.3f of peak)  all %.1f TFLOP/s" % (d["ms"], d.get("gemm_TFLOPs", 0), d.get("gemm_frac_of_peak", 0), d["achieved_TFLOPs"]))')
+    echo "[$arm] $* : $v" >> $out
+  done
+done
+cat $out
