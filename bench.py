@@ -195,7 +195,7 @@ def hbm_measured(dev):
     del a, b
     torch.cuda.empty_cache()
     return {"read_GBps": rd, "copy_GBps": cp, "torch_copy_GBps": 2 * 2 * n / (best * 1e-3) / 1e9,
-            "method": "bs_hbm_probe: 2 GiB, 16-B non-temporal loads, 4096 x 256 threads, best of 10, HIP events"}
+            "method": "bs_hbm_probe: 2 GiB, 16-B non-temporal loads (8 in flight per thread), 2048 x 256 threads, best of 10, HIP events"}
 
 
 def _cpu_model():
