@@ -752,8 +752,25 @@ __global__ __launch_bounds__(LB) void gemv_rows_kernel(const bf16* __restrict__ 
 // unit's MFMAs run.  Wave partials meet in LDS; the epilogue walks n fastest (coalesced stores,
 // and 16 aligned lanes = one 16-column argmax tile).
 // ------------------------------------------------------------------------------------
-template <int T, int MT, int WAVES>
-__global__ __launch_bounds__(WAVES * 64) void gemv_tiles_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
+// Weight-only int8 (WT = int8_t): a lane's 16 weights of a unit are 16 bytes, converted in registers to
+// two exact bf16x8 (|Q| <= 127; u = q ^ 0x80 through v_cvt_f32_ubyte*, minus 128) before the same MFMAs;
+// the row scale is the epilogue's col_scale.  Half the streamed bytes of the bf16 tiles, no dequant pass.
+__device__ __forceinline__ void q8x16_to_bf16(const u32x4v raw, bf16x8& lo, bf16x8& hi) {
+  const uint32_t v[4] = {raw.x ^ 0x80808080u, raw.y ^ 0x80808080u, raw.z ^ 0x80808080u, raw.w ^ 0x80808080u};
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    bf16x8& o = i ? hi : lo;
+    const uint32_t a = v[2 * i], b = v[2 * i + 1];
+    // (float)(byte) lowers to v_cvt_f32_ubyte{0..3}
+    o[0] = (bf16)((float)(a & 0xFF) - 128.f); o[1] = (bf16)((float)((a >> 8) & 0xFF) - 128.f);
+    o[2] = (bf16)((float)((a >> 16) & 0xFF) - 128.f); o[3] = (bf16)((float)(a >> 24) - 128.f);
+    o[4] = (bf16)((float)(b & 0xFF) - 128.f); o[5] = (bf16)((float)((b >> 8) & 0xFF) - 128.f);
+    o[6] = (bf16)((float)((b >> 16) & 0xFF) - 128.f); o[7] = (bf16)((float)(b >> 24) - 128.f);
+  }
+}
+
+template <int T, int MT, int WAVES, typename WT = bf16>
+__global__ __launch_bounds__(WAVES * 64) void gemv_tiles_kernel(const WT* __restrict__ W, const bf16* __restrict__ X,
                                                                 int M, int N, int K, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int RS = MT * 16 + 1;  // padded LDS row: [n][m]
@@ -767,7 +784,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_tiles_kernel(const bf16* __re
   const int ub0 = min(units_all, ks * upb), units = min(units_all, ub0 + upb) - ub0;
   const int per = (units + WAVES - 1) / WAVES;
   const int u0 = ub0 + min(units, w * per), u1 = ub0 + min(units, w * per + per);
-  const bf16* wp[T];
+  const WT* wp[T];
 #pragma unroll
   for (int t = 0; t < T; t++) wp[t] = W + (size_t)min(n0 + t * 16 + r, N - 1) * K + g * 16;
   const bf16* xp[MT];
@@ -783,8 +800,12 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_tiles_kernel(const bf16* __re
     const size_t o = (size_t)u * 64;
 #pragma unroll
     for (int t = 0; t < T; t++) {
-      aa[t][0] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[t] + o));
-      aa[t][1] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[t] + o + 8));
+      if constexpr (sizeof(WT) == 1) {
+        q8x16_to_bf16(__builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(wp[t] + o)), aa[t][0], aa[t][1]);
+      } else {
+        aa[t][0] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[t] + o));
+        aa[t][1] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[t] + o + 8));
+      }
     }
 #pragma unroll
     for (int mt = 0; mt < MT; mt++) {
@@ -882,11 +903,11 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_tiles_kernel(const bf16* __re
   });
 }
 
-template <int T, int MT, int WAVES>
-static void gemv_tiles_launch(const bf16* X, const bf16* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s) {
+template <int T, int MT, int WAVES, typename WT = bf16>
+static void gemv_tiles_launch(const bf16* X, const WT* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s) {
   const size_t shm = sizeof(float) * WAVES * (T * 16) * (MT * 16 + 1);
   const int blocks = (N + T * 16 - 1) / (T * 16);
-  gemv_tiles_kernel<T, MT, WAVES><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+  gemv_tiles_kernel<T, MT, WAVES, WT><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
 }
 
 // Shape choice: the BLOOM shapes take the fastest (tiles, K splits, waves) of the
@@ -901,7 +922,8 @@ static const TileCfg kTileTable[] = {
   {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 4, 4, 8, 4, 4, 8},
 };
 
-static bool gemv_tiles_dispatch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s) {
+template <typename WT = bf16>
+static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K, const Epi& ep, hipStream_t s) {
   if (M <= 4 || M > 32 || (K % 64) != 0) return false;
   const int units = K / 64;
   int T = N >= 16384 ? 4 : 2, KS = 1, WV = 0;
@@ -920,8 +942,8 @@ static bool gemv_tiles_dispatch(const bf16* x, const bf16* w, int M, int N, int 
   const bool two = M > 16;
   auto go = [&](auto tc, auto wc) {
     constexpr int TT = decltype(tc)::value, WW = decltype(wc)::value;
-    if (two) gemv_tiles_launch<TT, 2, WW>(x, w, M, N, K, KS, ep, s);
-    else gemv_tiles_launch<TT, 1, WW>(x, w, M, N, K, KS, ep, s);
+    if (two) gemv_tiles_launch<TT, 2, WW, WT>(x, w, M, N, K, KS, ep, s);
+    else gemv_tiles_launch<TT, 1, WW, WT>(x, w, M, N, K, KS, ep, s);
   };
   auto gw = [&](auto tc) {
     if (WV == 4) go(tc, EpiKindC<4>{});
@@ -2387,7 +2409,9 @@ void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* 
     else gemv_q8_launch<1, 8>(Q, scale, x, ln, M, N, K, e, s);
     return;
   }
-  // prefill / wide batches: dequantize to the bf16 scratch, then the bf16 GEMM (or batched GEMV)
+  // batched decode (8 < M <= 32): the int8 tile GEMV converts in registers (no dequant pass)
+  if (!gemv_tiles_disabled() && gemv_tiles_dispatch<int8_t>(x, Q, M, N, K, e, s)) return;
+  // prefill: dequantize to the bf16 scratch, then the bf16 GEMM
   launch_dequant_rows(Q, nullptr, w_scratch, N, K, s);
   launch_linear(1, X, w_scratch, M, N, K, e, s);
 }
