@@ -17,8 +17,8 @@ LIB = os.path.join(PKG, "lib", "libbloomstage.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "stage.hip", "codec.cpp"]
-HEADERS = ["common.h", "kernels.h", "attn_merge.h"]
+SOURCES = ["kernels.hip", "stage.hip", "codec.cpp", "safetensors.cpp"]
+HEADERS = ["common.h", "kernels.h", "attn_merge.h", "safetensors.h"]
 STAMP = os.path.join(OBJ, "build_id")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-Wno-unused-result", "-Wno-unused-value", f"-I{os.path.join(ROOT, 'include')}"]

@@ -18,6 +18,7 @@
 
 #include "../../include/bloomstage.h"
 #include "kernels.h"
+#include "safetensors.h"
 
 static thread_local std::string g_err;
 
@@ -166,7 +167,7 @@ static void alibi_slopes(int n_head, float* out) {
   }
 }
 
-static int validate(const bs_stage_desc* d) {
+static int validate(const bs_stage_desc* d, bool from_file = false) {
   if (!d) return fail(BS_ERR_INVALID, "desc is NULL");
   if (d->hidden <= 0 || d->n_head <= 0 || d->hidden % d->n_head)
     return fail(BS_ERR_INVALID, "hidden must be a positive multiple of n_head");
@@ -182,7 +183,7 @@ static int validate(const bs_stage_desc* d) {
   if (d->head_vocab_begin < 0 || d->head_vocab_end < d->head_vocab_begin || d->head_vocab_end > d->vocab ||
       d->head_vocab_begin % 16 || d->head_vocab_end % 16)
     return fail(BS_ERR_INVALID, "head vocab slice must be a 16-aligned sub-range of [0, vocab)");
-  if (d->weight_source != BS_WEIGHTS_SYNTHETIC && d->weight_source != BS_WEIGHTS_HOST)
+  if (!from_file && d->weight_source != BS_WEIGHTS_SYNTHETIC && d->weight_source != BS_WEIGHTS_HOST)
     return fail(BS_ERR_INVALID, "unknown weight_source");
   if (d->flags & ~BS_FLAG_INT8_WEIGHTS) return fail(BS_ERR_INVALID, "unknown desc flags");
   if ((d->flags & BS_FLAG_INT8_WEIGHTS) && d->dtype != BS_DT_BFLOAT16)
@@ -241,10 +242,116 @@ static void free_stage(bs_stage* s) {
   delete s;
 }
 
-extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
+// Checkpoint tensor of each canonical-order entry (the BS_WEIGHTS_HOST layout), HF BloomModel names
+// (modeling_bloom.py; the names the reference's ONNX modules were exported from).
+struct FileEntry {
+  std::string name;
+  uint64_t first;                // element offset inside the checkpoint tensor (head slice rows)
+  std::vector<int64_t> shape;    // the checkpoint tensor's expected shape
+};
+static std::vector<FileEntry> file_entries(const bs_stage_desc* d) {
+  const int64_t h = d->hidden, V = d->vocab;
+  std::vector<FileEntry> e;
+  if (d->is_first || d->is_last) e.push_back({"word_embeddings.weight", 0, {V, h}});
+  if (d->is_first) {
+    e.push_back({"word_embeddings_layernorm.weight", 0, {h}});
+    e.push_back({"word_embeddings_layernorm.bias", 0, {h}});
+  }
+  static const char* tn[T_NLAYER] = {
+      "input_layernorm.weight", "input_layernorm.bias", "self_attention.query_key_value.weight",
+      "self_attention.query_key_value.bias", "self_attention.dense.weight", "self_attention.dense.bias",
+      "post_attention_layernorm.weight", "post_attention_layernorm.bias", "mlp.dense_h_to_4h.weight",
+      "mlp.dense_h_to_4h.bias", "mlp.dense_4h_to_h.weight", "mlp.dense_4h_to_h.bias"};
+  const std::vector<int64_t> ts[T_NLAYER] = {{h}, {h}, {3 * h, h}, {3 * h}, {h, h}, {h}, {h}, {h}, {4 * h, h}, {4 * h},
+                                             {h, 4 * h}, {h}};
+  for (int l = d->layer_begin; l < d->layer_end; l++)
+    for (int t = 0; t < T_NLAYER; t++) e.push_back({"h." + std::to_string(l) + "." + tn[t], 0, ts[t]});
+  if (d->is_last) { e.push_back({"ln_f.weight", 0, {h}}); e.push_back({"ln_f.bias", 0, {h}}); }
+  const bool slice = d->head_vocab_end > d->head_vocab_begin;
+  if (slice && !d->is_first && !d->is_last) e.push_back({"word_embeddings.weight", (uint64_t)d->head_vocab_begin * h, {V, h}});
+  if (slice && !d->is_last) { e.push_back({"ln_f.weight", 0, {h}}); e.push_back({"ln_f.bias", 0, {h}}); }
+  return e;
+}
+static const st::Tensor* find_entry(const st::Checkpoint& ck, const FileEntry& fe, std::string* why) {
+  const st::Tensor* t = ck.find(fe.name);
+  if (!t && fe.name == "word_embeddings.weight") t = ck.find("lm_head.weight");  // tied head saved alone
+  if (!t) { *why = "checkpoint has no tensor '" + fe.name + "'"; return nullptr; }
+  if (t->shape != fe.shape) {
+    std::string a, b;
+    for (auto v : t->shape) a += std::to_string(v) + ",";
+    for (auto v : fe.shape) b += std::to_string(v) + ",";
+    *why = "tensor '" + fe.name + "' has shape [" + a + "] but the stage needs [" + b + "]";
+    return nullptr;
+  }
+  if (t->dtype == st::OTHER) { *why = "tensor '" + fe.name + "' has dtype " + t->dtype_name + " (need F32/F16/BF16)"; return nullptr; }
+  return t;
+}
+
+static float host_f16(uint16_t v) {
+  const uint32_t sgn = (uint32_t)(v >> 15) << 31, ex = (v >> 10) & 31, man = v & 1023;
+  uint32_t bits;
+  if (ex == 31) bits = sgn | 0x7F800000u | (man << 13);
+  else if (ex) bits = sgn | ((ex + 112) << 23) | (man << 13);
+  else if (!man) bits = sgn;
+  else {  // subnormal: exact in fp32
+    float f = (float)man * 5.9604644775390625e-8f;  // 2^-24
+    std::memcpy(&bits, &f, 4);
+    bits |= sgn;
+  }
+  float f;
+  std::memcpy(&f, &bits, 4);
+  return f;
+}
+
+static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Checkpoint* ck);
+
+extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) { return init_stage(desc, out, nullptr); }
+
+extern "C" int bs_init_stage_file(const bs_stage_desc* desc, const char* path, bs_stage** out) {
   if (!out) return fail(BS_ERR_INVALID, "out is NULL");
   *out = nullptr;
-  int rc = validate(desc);
+  if (!path) return fail(BS_ERR_INVALID, "path is NULL");
+  int rc = validate(desc, true);
+  if (rc) return rc;
+  st::Checkpoint ck;
+  std::string err;
+  if (!ck.open(path, &err)) return fail(BS_ERR_INVALID, err);
+  for (const auto& fe : file_entries(desc))  // every tensor present and shaped right before any allocation
+    if (!find_entry(ck, fe, &err)) return fail(BS_ERR_INVALID, err);
+  return init_stage(desc, out, &ck);
+}
+
+extern "C" int bs_weights_file_probe(const char* path, int32_t* hidden, int32_t* n_layer, int32_t* vocab) {
+  if (!path) return fail(BS_ERR_INVALID, "path is NULL");
+  st::Checkpoint ck;
+  std::string err;
+  if (!ck.open(path, &err)) return fail(BS_ERR_INVALID, err);
+  const st::Tensor* e = ck.find("word_embeddings.weight");
+  if (!e) e = ck.find("lm_head.weight");
+  int32_t hid = -1, nl = 0, V = -1;
+  if (e && e->shape.size() == 2) { V = (int32_t)e->shape[0]; hid = (int32_t)e->shape[1]; }
+  for (const auto& kv : ck.tensors()) {  // layers: 1 + the highest h.<i>. present
+    const std::string& n = kv.first;
+    auto ends = [&](const std::string& x) { return n.size() >= x.size() && !n.compare(n.size() - x.size(), x.size(), x); };
+    if (hid < 0 && (ends("layernorm.weight") || ends("ln_f.weight")) && kv.second.shape.size() == 1)
+      hid = (int32_t)kv.second.shape[0];  // any LayerNorm gives the width
+    size_t p = n.rfind("h.", 0) == 0 ? 2 : (n.rfind("transformer.h.", 0) == 0 ? 14 : std::string::npos);
+    if (p == std::string::npos) continue;
+    long i = 0;
+    size_t q = p;
+    while (q < n.size() && n[q] >= '0' && n[q] <= '9' && i < 1000000) i = i * 10 + (n[q++] - '0');
+    if (q > p && q < n.size() && n[q] == '.') nl = std::max(nl, (int32_t)i + 1);
+  }
+  if (hidden) *hidden = hid;
+  if (n_layer) *n_layer = nl;
+  if (vocab) *vocab = V;
+  return BS_OK;
+}
+
+static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Checkpoint* ck) {
+  if (!out) return fail(BS_ERR_INVALID, "out is NULL");
+  *out = nullptr;
+  int rc = validate(desc, ck != nullptr);
   if (rc) return rc;
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
@@ -334,7 +441,65 @@ extern "C" int bs_init_stage(const bs_stage_desc* desc, bs_stage** out) {
   };
 
   // ---- weights
-  if (desc->weight_source == BS_WEIGHTS_SYNTHETIC) {
+  if (ck) {
+    // Straight from the file mapping: matching dtypes are copied as they are, others widen to fp32 on
+    // the host (exact) and take the BS_WEIGHTS_HOST conversion, so a file of fp32 weights loads
+    // bit-identical to the same weights passed as a host buffer.
+    const std::vector<FileEntry> fes = file_entries(desc);
+    if (fes.size() != s->order.size()) return cleanup(fail(BS_ERR_STATE, "checkpoint entry list out of step"));
+    const size_t chunk = 16u << 20;
+    std::vector<float> wide(chunk);
+    float* bounce = nullptr;
+    if (hipMalloc(&bounce, chunk * sizeof(float)) != hipSuccess) return cleanup(fail(BS_ERR_OOM, "bounce alloc"));
+    std::string why;
+    for (size_t oi2 = 0; oi2 < s->order.size(); oi2++) {
+      const auto& o = s->order[oi2];
+      const bool q = s->order_q8[oi2].first != nullptr;
+      char* dst = (char*)(q ? s->wtmp : o.first);
+      const st::Tensor* t = find_entry(*ck, fes[oi2], &why);
+      if (!t || fes[oi2].first + o.second > t->numel()) {
+        hipFree(bounce);
+        return cleanup(fail(BS_ERR_INVALID, t ? "head slice outside the checkpoint's embedding" : why));
+      }
+      const bool same = (s->bf16 && t->dtype == st::BF16) || (!s->bf16 && t->dtype == st::F32);
+      const size_t tes = t->dtype == st::F32 ? 4 : 2;
+      const uint8_t* src = t->data + fes[oi2].first * tes;
+      bool ok = true;
+      if (same) {
+        ok = hipMemcpyAsync(dst, src, o.second * s->esz, hipMemcpyHostToDevice, s->own) == hipSuccess;
+      } else {
+        for (size_t i = 0; ok && i < o.second; i += chunk) {
+          const size_t n = std::min(chunk, o.second - i);
+          const uint8_t* p = src + i * tes;
+          if (t->dtype == st::F32) {
+            std::memcpy(wide.data(), p, n * 4);
+          } else {
+            for (size_t j = 0; j < n; j++) {
+              uint16_t v;
+              std::memcpy(&v, p + 2 * j, 2);
+              if (t->dtype == st::BF16) {
+                const uint32_t b = (uint32_t)v << 16;
+                std::memcpy(&wide[j], &b, 4);
+              } else {
+                wide[j] = host_f16(v);
+              }
+            }
+          }
+          ok = hipMemcpyAsync(bounce, wide.data(), n * sizeof(float), hipMemcpyHostToDevice, s->own) == hipSuccess;
+          if (ok) launch_convert_f32(dst + i * s->esz, s->bf16, bounce, n, s->own);
+          ok = ok && hipStreamSynchronize(s->own) == hipSuccess;  // `wide` is refilled next round
+        }
+      }
+      if (ok && q) quantize(oi2);
+      if (!ok) {
+        hipFree(bounce);
+        return cleanup(fail(BS_ERR_DEVICE, "weight upload failed"));
+      }
+    }
+    const bool synced = hipStreamSynchronize(s->own) == hipSuccess;  // the mapping goes away after init
+    hipFree(bounce);
+    if (!synced) return cleanup(fail(BS_ERR_DEVICE, "weight upload failed"));
+  } else if (desc->weight_source == BS_WEIGHTS_SYNTHETIC) {
     const uint64_t seed = desc->seed;
     if (s->wemb) launch_gen_fill(s->wemb, s->bf16, V * h, tensor_key(seed, -1, M_WEMB), 0, s->own);
     if (s->emb_g) launch_gen_fill(s->emb_g, s->bf16, h, tensor_key(seed, -1, M_EMB_G), 2, s->own);

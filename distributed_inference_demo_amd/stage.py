@@ -81,7 +81,7 @@ EXPORTS = [
     "bs_stage_weight_count", "bs_abi_version", "bs_profile_enable", "bs_profile_read",
     "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
     "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice", "bs_stream_delay", "bs_set_sampling",
-    "bs_build_id", "bs_hbm_probe",
+    "bs_build_id", "bs_hbm_probe", "bs_init_stage_file", "bs_weights_file_probe",
 ]
 
 _LIB = None
@@ -105,6 +105,8 @@ def lib():
             raise BloomStageError(f"{LIB_PATH} was built from other sources (stamp {got[:12]}, sources {want[:12]}): "
                                   "rebuild with `python -m distributed_inference_demo_amd.build`")
         L.bs_init_stage.argtypes = [ctypes.POINTER(StageDesc), ctypes.POINTER(vp)]
+        L.bs_init_stage_file.argtypes = [ctypes.POINTER(StageDesc), ctypes.c_char_p, ctypes.POINTER(vp)]
+        L.bs_weights_file_probe.argtypes = [ctypes.c_char_p] + [ctypes.POINTER(i32)] * 3
         L.bs_forward.argtypes = [vp, ctypes.POINTER(Step), vp, vp, vp, vp]
         L.bs_reset_kv.argtypes = [vp, i32]
         L.bs_release.argtypes = [vp]
@@ -167,7 +169,11 @@ class Stage:
 
     def __init__(self, hidden, n_head, n_layer, vocab, layer_begin, layer_end, *, dtype="bf16", device=0,
                  max_batch=1, max_ctx=2048, max_tokens=0, seed=0, eps=1e-5, host_weights=None,
-                 is_first=None, is_last=None, head_slice=None, int8_weights=False):
+                 is_first=None, is_last=None, head_slice=None, int8_weights=False, weights_file=None):
+        """weights_file: a safetensors checkpoint (or its sharded *.index.json) of HF BLOOM tensors;
+        the stage maps it and loads only its own layer range (bs_init_stage_file)."""
+        if weights_file is not None and host_weights is not None:
+            raise ValueError("pass host_weights or weights_file, not both")
         d = StageDesc()
         d.hidden, d.n_head, d.n_layer, d.vocab, d.ln_eps = hidden, n_head, n_layer, vocab, eps
         d.layer_begin, d.layer_end = layer_begin, layer_end
@@ -193,7 +199,10 @@ class Stage:
         self.is_first, self.is_last = bool(d.is_first), bool(d.is_last)
         self.max_batch, self.max_ctx = max_batch, max_ctx
         h = ctypes.c_void_p()
-        _check(lib().bs_init_stage(ctypes.byref(d), ctypes.byref(h)))
+        if weights_file is not None:
+            _check(lib().bs_init_stage_file(ctypes.byref(d), os.fsencode(weights_file), ctypes.byref(h)))
+        else:
+            _check(lib().bs_init_stage(ctypes.byref(d), ctypes.byref(h)))
         self._h = h
         self._weights_ref = None  # uploaded; host copy no longer needed
         self.past = [0] * max_batch  # host mirror of cached positions per KV row
@@ -313,6 +322,13 @@ def hbm_probe(device=0, nbytes=2 << 30):
     r, c = ctypes.c_double(), ctypes.c_double()
     _check(lib().bs_hbm_probe(device, nbytes, ctypes.byref(r), ctypes.byref(c)))
     return r.value, c.value
+
+
+def probe_weights_file(path):
+    """(hidden, n_layer, vocab) a checkpoint implies (bs_weights_file_probe); -1 where unknown."""
+    v = [ctypes.c_int32() for _ in range(3)]
+    _check(lib().bs_weights_file_probe(os.fsencode(path), *[ctypes.byref(x) for x in v]))
+    return tuple(x.value for x in v)
 
 
 def weight_count(**kw):

@@ -115,6 +115,19 @@ typedef struct bs_step {
 /* Create a stage on desc->device: allocates weights, KV cache and workspace in HBM. */
 int bs_init_stage(const bs_stage_desc *desc, bs_stage **out);
 
+/* createSession(model_path) (native-lib.cpp:671-678 -> SessionCache, session_cache.h:26-35): create a
+ * stage whose weights come from a checkpoint file instead of desc->weight_source.  `path` is a
+ * safetensors file or a sharded checkpoint's *.index.json ({"weight_map": {name: shard}}, shards
+ * beside it) holding HF BloomModel tensors ("h.<i>.self_attention.query_key_value.weight", ...;
+ * a "transformer." prefix is accepted; "lm_head.weight" stands in for a missing
+ * "word_embeddings.weight").  The file is memory-mapped and only the stage's own tensors are read;
+ * F32/F16/BF16 are accepted and stored in desc->dtype (bf16 from fp32 rounds to nearest even,
+ * exactly as BS_WEIGHTS_HOST).  A missing or mis-shaped tensor fails before any allocation. */
+int bs_init_stage_file(const bs_stage_desc *desc, const char *path, bs_stage **out);
+/* Model dimensions a checkpoint implies (hidden and vocab from word_embeddings, n_layer = 1 + the
+ * highest block index); -1 where the file does not say.  Host only, no device needed. */
+int bs_weights_file_probe(const char *path, int32_t *hidden, int32_t *n_layer, int32_t *vocab);
+
 /* Stage forward, stream-ordered on `stream` (hipStream_t, NULL = the stage's own stream).
  *  in : first stage -> int32 token ids [B][S]; otherwise fp32 hidden [B][S][hidden]
  *  out: last stage  -> int32 token ids [B] (greedy argmax of each row's last position);
