@@ -1,6 +1,6 @@
 """Vendor-library reference point for the prefill GEMM shapes: torch.nn.functional.linear (bf16,
 hipBLASLt on ROCm) on bloom-1b1 / 3b / 7b1 prefill projections, device time per call from HIP
-events over back-to-back launches.  A measurement aid for DESIGN.md (what the library reaches on
+events over hipGraph replays of 20 back-to-back calls.  A measurement aid for DESIGN.md (what the library reaches on
 the same M = 512 shapes our gemm_mfma2_kernel runs), not part of the product path.
 
     python tools/gemm_shapes_torch.py [M]
@@ -26,14 +26,24 @@ def main():
             for _ in range(20):
                 F.linear(x, w, b)
             torch.cuda.synchronize()
-            reps = 200
+            # captured in a graph: host launch cost (~10-20 us per F.linear call) would otherwise
+            # be what the events measure at these sizes
+            per, reps = 20, 20
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side):
+                    for _ in range(per):
+                        F.linear(x, w, b)
+            g.replay()
+            torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(reps):
-                F.linear(x, w, b)
+                g.replay()
             e1.record()
             torch.cuda.synchronize()
-            s = e0.elapsed_time(e1) / 1e3 / reps
+            s = e0.elapsed_time(e1) / 1e3 / (reps * per)
             flop = 2.0 * M * n * k
             if name == "bloom-1b1":
                 tot_flop += flop
