@@ -38,13 +38,6 @@ struct Epi {
   unsigned* sk_tickets;
   size_t sk_cap;
   int sk_ntickets;
-  // stream-K workspace of the prefill GEMM (gemm_sk): fp32 partial tiles, two per workgroup of the
-  // grid (capacity in floats), and one arrival ticket per output tile (zero between launches).
-  // Null: the GEMM keeps one workgroup per output tile.
-  float* gsk_ws;
-  unsigned* gsk_tickets;
-  size_t gsk_cap;
-  int gsk_ntickets;
   // int8 weights: y[m][n] *= col_scale[n] before the epilogue (the weight operand held Q, not
   // Q * scale).  Null otherwise.  Not applied by EPI_ARGMAX.
   const float* col_scale;

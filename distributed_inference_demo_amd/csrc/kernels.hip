@@ -1091,23 +1091,10 @@ struct GemmEpiPre {
   int past[EK == EPI_QKV ? TM * 4 : 1];
 };
 
-template <int BM, int BN, int PS, int EK>
-__global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
-                                                         int M, int N, int K, Epi ep, int xcd) {
-  constexpr int BK = 64;
-  constexpr int TM = BM / 32, TN = BN / 32;           // 16x16 tiles per wave (wave = BM/2 x BN/2)
-  constexpr int CA = BM * BK / 8 / 256, CB = BN * BK / 8 / 256;  // 16-B chunks per thread: 4, 4|2|1
-  __shared__ __attribute__((aligned(16))) bf16 As[2][BM * BK];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * BK];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1, r = lane & 15, g = lane >> 4;
-  int m0, n0;
-  gemm_tile_xcd(BM, BN, xcd, m0, n0);
-  auto sw = [](int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); };  // element offset
-  auto row_m = [&](int i, int e) { return m0 + wm * (BM / 2) + i * 16 + 4 * g + e; };
-  auto col_n = [&](int j) { return n0 + wn * (BN / 2) + j * 16 + r; };
-
-  GemmEpiPre<TM, TN, EK> pre;
+// row_m(i, e) / col_n(j): the output row / column of accumulator element e of fragment (i, j).
+template <int TM, int TN, int EK, typename RM, typename CN>
+__device__ __forceinline__ void gemm_epi_prefetch(GemmEpiPre<TM, TN, EK>& pre, const Epi& ep, int M, int N, RM row_m,
+                                                  CN col_n) {
   if constexpr (EK != EPI_ARGMAX) {
 #pragma unroll
     for (int j = 0; j < TN; j++) {
@@ -1132,6 +1119,72 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
           pre.past[i * 4 + e] = ep.past_dev ? ep.past_dev[min(row_m(i, e), M - 1) / ep.seq] : ep.past;
     }
   }
+}
+
+template <int TM, int TN, int EK, typename RM, typename CN>
+__device__ __forceinline__ void gemm_epi_store(const f32x4 (&acc)[TM][TN], const GemmEpiPre<TM, TN, EK>& pre,
+                                               const Epi& ep, int M, int N, RM row_m, CN col_n) {
+  const int ntiles = (N + 15) >> 4;
+  if constexpr (EK == EPI_ARGMAX) {
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+      for (int j = 0; j < TN; j++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const int m = row_m(i, e), n = col_n(j);
+          epi_apply<bf16, EK>(ep, m, n, acc[i][j][e], m < M && n < N, ntiles);
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int m = row_m(i, e);
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+          const int n = col_n(j);
+          if (m >= M || n >= N) continue;
+          const float v = acc[i][j][e] * pre.cscale[j] + pre.bias[j];
+          if constexpr (EK == EPI_QKV) {
+            const int three = 3 * ep.head_dim;
+            const int head = n / three, rr = n - head * three, which = rr / ep.head_dim, d = rr - which * ep.head_dim;
+            if (which == 0) {
+              ((bf16*)ep.q_out)[(size_t)m * ep.hidden + head * ep.head_dim + d] = from_f32<bf16>(v);
+            } else {
+              const int b = m / ep.seq, t = m - b * ep.seq;
+              const size_t idx =
+                  (((size_t)(ep.slot + b) * ep.n_head + head) * ep.max_ctx + pre.past[i * 4 + e] + t) * ep.head_dim + d;
+              ((bf16*)(which == 1 ? ep.k_cache : ep.v_cache))[idx] = from_f32<bf16>(v);
+            }
+          } else if constexpr (EK == EPI_RESID) {
+            ep.out_f32[(size_t)m * ep.ldo + n] = v + pre.resid[(i * 4 + e) * TN + j];
+          } else {
+            ((bf16*)ep.out_act)[(size_t)m * ep.ldo + n] = from_f32<bf16>(gelu_bloom(v));
+          }
+        }
+      }
+  }
+}
+
+template <int BM, int BN, int PS, int EK>
+__global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
+                                                         int M, int N, int K, Epi ep, int xcd) {
+  constexpr int BK = 64;
+  constexpr int TM = BM / 32, TN = BN / 32;           // 16x16 tiles per wave (wave = BM/2 x BN/2)
+  constexpr int CA = BM * BK / 8 / 256, CB = BN * BK / 8 / 256;  // 16-B chunks per thread: 4, 4|2|1
+  __shared__ __attribute__((aligned(16))) bf16 As[2][BM * BK];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * BK];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1, r = lane & 15, g = lane >> 4;
+  int m0, n0;
+  gemm_tile_xcd(BM, BN, xcd, m0, n0);
+  auto sw = [](int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); };  // element offset
+  auto row_m = [&](int i, int e) { return m0 + wm * (BM / 2) + i * 16 + 4 * g + e; };
+  auto col_n = [&](int j) { return n0 + wn * (BN / 2) + j * 16 + r; };
+
+  GemmEpiPre<TM, TN, EK> pre;
+  gemm_epi_prefetch(pre, ep, M, N, row_m, col_n);
 
   const bf16* ga[CA]; const bf16* gb[CB];
   int la[CA], lb[CB];
@@ -1216,47 +1269,7 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
       cur ^= 1;
     }
   }
-  const int ntiles = (N + 15) >> 4;
-  if constexpr (EK == EPI_ARGMAX) {
-#pragma unroll
-    for (int i = 0; i < TM; i++)
-#pragma unroll
-      for (int j = 0; j < TN; j++)
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-          const int m = row_m(i, e), n = col_n(j);
-          epi_apply<bf16, EK>(ep, m, n, acc[i][j][e], m < M && n < N, ntiles);
-        }
-  } else {
-#pragma unroll
-    for (int i = 0; i < TM; i++)
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const int m = row_m(i, e);
-#pragma unroll
-        for (int j = 0; j < TN; j++) {
-          const int n = col_n(j);
-          if (m >= M || n >= N) continue;
-          const float v = acc[i][j][e] * pre.cscale[j] + pre.bias[j];
-          if constexpr (EK == EPI_QKV) {
-            const int three = 3 * ep.head_dim;
-            const int head = n / three, rr = n - head * three, which = rr / ep.head_dim, d = rr - which * ep.head_dim;
-            if (which == 0) {
-              ((bf16*)ep.q_out)[(size_t)m * ep.hidden + head * ep.head_dim + d] = from_f32<bf16>(v);
-            } else {
-              const int b = m / ep.seq, t = m - b * ep.seq;
-              const size_t idx =
-                  (((size_t)(ep.slot + b) * ep.n_head + head) * ep.max_ctx + pre.past[i * 4 + e] + t) * ep.head_dim + d;
-              ((bf16*)(which == 1 ? ep.k_cache : ep.v_cache))[idx] = from_f32<bf16>(v);
-            }
-          } else if constexpr (EK == EPI_RESID) {
-            ep.out_f32[(size_t)m * ep.ldo + n] = v + pre.resid[(i * 4 + e) * TN + j];
-          } else {
-            ((bf16*)ep.out_act)[(size_t)m * ep.ldo + n] = from_f32<bf16>(gelu_bloom(v));
-          }
-        }
-      }
-  }
+  gemm_epi_store(acc, pre, ep, M, N, row_m, col_n);
 }
 
 // gemm_mfma2_kernel with the epilogue kind as a template argument.
@@ -1268,176 +1281,6 @@ static void gemm2_launch(const bf16* x, const bf16* w, int M, int N, int K, cons
     case EPI_RESID: gemm_mfma2_kernel<BM, BN, PS, EPI_RESID><<<grid, 256, 0, s>>>(x, w, M, N, K, ep, xcd); break;
     case EPI_GELU: gemm_mfma2_kernel<BM, BN, PS, EPI_GELU><<<grid, 256, 0, s>>>(x, w, M, N, K, ep, xcd); break;
     default: gemm_mfma2_kernel<BM, BN, PS, EPI_ARGMAX><<<grid, 256, 0, s>>>(x, w, M, N, K, ep, xcd); break;
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// gemm_sk: stream-K prefill GEMM.  At prefill sizes (bloom-1b1, 512 tokens: 144-192 128x128 tiles
-// for QKV / fc1, 48 for dense / fc2) one workgroup per output tile leaves most of the 256 CUs idle or
-// forces small, low-intensity tiles (64x64: 32 FLOP per L2 byte, LDS-write bound).  Here a fixed grid
-// of G workgroups (2 per CU) splits the tiles x K-steps iteration space into G equal contiguous ranges:
-// every CU gets the same MFMA work whatever the tile count, on 128x128 tiles (64 FLOP per L2 byte,
-// 2x2 waves of 64x64).  A tile split between workgroups is combined by its last arriver: each
-// contributor stores its fp32 partial (write-through, sc1), takes the tile's ticket, and the one that
-// draws the last ticket sums every contributor's partial in contributor order (deterministic, whoever
-// arrives last) and runs the epilogue.  Nobody waits on another workgroup, so residency is never
-// assumed.  Logical workgroup ids are remapped XCD-major (dispatch puts workgroup b on XCD b % 8), so
-// consecutive ranges -- the tiles sharing X rows and the contributors of one tile -- sit on one XCD.
-// The K loop is gemm_mfma2's one-tile-lookahead register-staged loop (BK = 64).
-// ------------------------------------------------------------------------------------
-struct SkGrid {
-  int tiles_n;   // tiles along N
-  int nk;        // K-steps per tile (K / 64)
-  long total;    // tiles * nk
-  int G;         // workgroups (multiple of 8)
-};
-
-__device__ __forceinline__ int sk_owner(long i, const SkGrid& g) {  // logical workgroup owning iteration i
-  return (int)(((i + 1) * g.G + g.total - 1) / g.total) - 1;
-}
-
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void gemm_sk_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W, int M,
-                                                      int N, int K, Epi ep, SkGrid g) {
-  constexpr int BK = 64;
-  constexpr int TM = BM / 32, TN = BN / 32;
-  constexpr int CA = BM * BK / 8 / 256, CB = BN * BK / 8 / 256;
-  constexpr int NF = TM * TN;  // f32x4 fragments per thread
-  __shared__ __attribute__((aligned(16))) bf16 As[2][BM * BK];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * BK];
-  __shared__ int sk_last;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1, r = lane & 15, gq = lane >> 4;
-  auto sw = [](int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); };
-  const int lb = (blockIdx.x & 7) * (g.G >> 3) + (blockIdx.x >> 3);  // XCD-major logical id
-  const long beg = (long)lb * g.total / g.G, end = (long)(lb + 1) * g.total / g.G;
-  const int ntiles16 = (N + 15) >> 4;
-  const __amdgpu_buffer_rsrc_t slab = attn_rsrc(ep.gsk_ws);
-
-  for (long it = beg; it < end;) {
-    const int tile = (int)(it / g.nk), k0 = (int)(it - (long)tile * g.nk);
-    const int k1 = (int)min((long)g.nk, k0 + (end - it));
-    const int m0 = (tile / g.tiles_n) * BM, n0 = (tile % g.tiles_n) * BN;
-    const bf16* ga[CA]; const bf16* gb[CB];
-    int la[CA], lbo[CB];
-#pragma unroll
-    for (int i = 0; i < CA; i++) {
-      const int c = tid + i * 256, row = c >> 3, ch = c & 7;
-      ga[i] = X + (size_t)min(m0 + row, M - 1) * K + (size_t)k0 * BK + ch * 8;
-      la[i] = sw(row, ch);
-    }
-#pragma unroll
-    for (int i = 0; i < CB; i++) {
-      const int c = tid + i * 256, row = c >> 3, ch = c & 7;
-      gb[i] = W + (size_t)min(n0 + row, N - 1) * K + (size_t)k0 * BK + ch * 8;
-      lbo[i] = sw(row, ch);
-    }
-    bf16x8 ra[CA], rb[CB];
-    auto gload = [&](int kt) {
-      const size_t off = (size_t)kt * BK;
-#pragma unroll
-      for (int i = 0; i < CA; i++) ra[i] = *reinterpret_cast<const bf16x8*>(ga[i] + off);
-#pragma unroll
-      for (int i = 0; i < CB; i++) rb[i] = *reinterpret_cast<const bf16x8*>(gb[i] + off);
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-      for (int i = 0; i < CA; i++) *reinterpret_cast<bf16x8*>(&As[buf][la[i]]) = ra[i];
-#pragma unroll
-      for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(&Bs[buf][lbo[i]]) = rb[i];
-    };
-    f32x4 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; i++)
-#pragma unroll
-      for (int j = 0; j < TN; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int nkt = k1 - k0;
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    int cur = 0;
-    for (int kt = 0; kt < nkt; kt++) {
-      const bool more = kt + 1 < nkt;
-      if (more) gload(kt + 1);
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ks++) {
-        bf16x8 af[TM], bfr[TN];
-#pragma unroll
-        for (int i = 0; i < TM; i++)
-          af[i] = *reinterpret_cast<const bf16x8*>(&As[cur][sw(wm * (BM / 2) + i * 16 + r, ks * 4 + gq)]);
-#pragma unroll
-        for (int j = 0; j < TN; j++)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][sw(wn * (BN / 2) + j * 16 + r, ks * 4 + gq)]);
-#pragma unroll
-        for (int i = 0; i < TM; i++)
-#pragma unroll
-          for (int j = 0; j < TN; j++)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      }
-      if (more) lstore(cur ^ 1);
-      __syncthreads();
-      cur ^= 1;
-    }
-
-    bool run_epi = true;
-    if (k0 != 0 || k1 != g.nk) {  // a split tile: publish, take the ticket, the last arriver combines
-      const int slot = it == beg ? 0 : 1;  // a workgroup's split segments: its first and its last
-      const uint32_t base = (uint32_t)((lb * 2 + slot) * NF) * 256u * 16u;
-#pragma unroll
-      for (int i = 0; i < TM; i++)
-#pragma unroll
-        for (int j = 0; j < TN; j++) {
-          u32x4v v;
-          for (int e = 0; e < 4; e++) v[e] = __float_as_uint(acc[i][j][e]);
-          __builtin_amdgcn_raw_buffer_store_b128(v, slab, base + (uint32_t)((i * TN + j) * 256 + tid) * 16u, 0, 16);
-        }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const int c0 = sk_owner((long)tile * g.nk, g), c1 = sk_owner((long)tile * g.nk + g.nk - 1, g);
-      if (tid == 0) {
-        typedef __attribute__((address_space(1))) unsigned gu32;
-        const unsigned old =
-            __hip_atomic_fetch_add((gu32*)(ep.gsk_tickets + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sk_last = old == (unsigned)(c1 - c0);
-        if (sk_last) __hip_atomic_store((gu32*)(ep.gsk_tickets + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      run_epi = sk_last;
-      if (run_epi) {
-        // contributor c holds this tile in its first slot iff its range starts inside the tile
-        for (int i = 0; i < TM; i++)
-          for (int j = 0; j < TN; j++) {
-            f32x4 sum = (f32x4){0.f, 0.f, 0.f, 0.f};
-            for (int c = c0; c <= c1; c++) {
-              if (c == lb) {
-                sum += acc[i][j];
-              } else {
-                const int cs = ((long)c * g.total / g.G) >= (long)tile * g.nk ? 0 : 1;
-                const uint32_t off = (uint32_t)((c * 2 + cs) * NF + i * TN + j) * 256u * 16u + (uint32_t)tid * 16u;
-                const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(slab, off, 0, 16);
-                for (int e = 0; e < 4; e++) sum[e] += __uint_as_float(v[e]);
-              }
-            }
-            acc[i][j] = sum;
-          }
-      }
-    }
-    if (run_epi) {
-      epi_dispatch(ep.kind, [&](auto kc) {
-        constexpr int EK = decltype(kc)::value;
-#pragma unroll
-        for (int i = 0; i < TM; i++)
-#pragma unroll
-          for (int j = 0; j < TN; j++)
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-              const int m = m0 + wm * (BM / 2) + i * 16 + 4 * gq + e;
-              const int n = n0 + wn * (BN / 2) + j * 16 + r;
-              epi_apply<bf16, EK>(ep, m, n, acc[i][j][e], m < M && n < N, ntiles16);
-            }
-      });
-    }
-    it += k1 - k0;
   }
 }
 
@@ -1482,21 +1325,6 @@ static bool gemm_no_narrow() {  // BS_GEMM_NO_NARROW=1: keep 64x64 prefill tiles
   static int v = -1;
   if (v < 0) { const char* e = getenv("BS_GEMM_NO_NARROW"); v = (e && *e && *e != '0') ? 1 : 0; }
   return v == 1;
-}
-
-// Stream-K prefill GEMM (gemm_sk_kernel) when the 128x128 tiles do not give every CU >= 2 tiles
-// of its own, K is whole 64-deep steps and the stage provided the workspace.  BS_GEMM_SK=0: off (A/B).
-static bool gemm_sk_dispatch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s) {
-  static const int mode = [] { const char* e = getenv("BS_GEMM_SK"); return e && *e ? atoi(e) : 0; }();
-  static const int grid = [] { const char* e = getenv("BS_GEMM_SK_G"); return e && *e ? atoi(e) : 512; }();
-  if (mode == 0 || !ep.gsk_ws || !ep.gsk_tickets || (K % 64) != 0) return false;
-  const int tm = (M + 127) / 128, tn = (N + 127) / 128, tiles = tm * tn;
-  if (tiles >= 512 || tiles > ep.gsk_ntickets) return false;
-  SkGrid g{tn, K / 64, (long)tiles * (K / 64), std::max(8, grid / 8 * 8)};
-  if (g.total < g.G) g.G = (int)std::max(8L, g.total / 8 * 8);
-  if ((size_t)g.G * 2 * 128 * 128 > ep.gsk_cap) return false;
-  gemm_sk_kernel<128, 128><<<g.G, 256, 0, s>>>(x, w, M, N, K, ep, g);
-  return true;
 }
 
 static bool gemv_rows_disabled() {
@@ -1688,7 +1516,6 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
       const char* e = getenv("BS_GEMM_TILE");
       return e && *e ? atoi(e) : 0;
     }();
-    if (forced == 0 && gemm_sk_dispatch(x, w, M, N, K, ep, s)) return;
     if (forced == 1) {
       gemm2_launch<128, 128, 1>(x, w, M, N, K, ep, s, gemm_xcd());
     } else if (forced == 2) {

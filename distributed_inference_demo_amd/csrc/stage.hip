@@ -73,10 +73,6 @@ struct ProfClass {
 // (one stream per stage); head slices on another stream never split K.
 constexpr size_t kSkCap = (size_t)16 * 32 * 4096;
 constexpr int kSkTickets = 4096;
-// stream-K prefill GEMM workspace (kernels.hip gemm_sk): 2 fp32 128x128 partial tiles for each of up
-// to 512 workgroups, one ticket per output tile
-constexpr size_t kGskCap = (size_t)512 * 2 * 128 * 128;
-constexpr int kGskTickets = 512;
 
 struct bs_stage {
   bs_stage_desc d;
@@ -121,8 +117,6 @@ struct bs_stage {
   unsigned* att_tickets = nullptr;     // [max_batch][n_head]
   float* sk_ws = nullptr;              // batched-GEMV split-K partials (kSkCap floats)
   unsigned* sk_tickets = nullptr;      // [kSkTickets]
-  float* gsk_ws = nullptr;             // stream-K prefill GEMM partials (kGskCap floats; prefill stages)
-  unsigned* gsk_tickets = nullptr;     // [kGskTickets]
   ProfClass prof;
   std::vector<std::pair<void*, size_t>> order;  // canonical weight order (BS_WEIGHTS_HOST layout)
   std::vector<std::pair<const float*, int>> order_q8;  // per order entry: (row scales, K) if int8, else (null, 0)
@@ -583,8 +577,6 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   wadd((size_t)desc->max_batch * desc->n_head * 4);  // attention split-merge tickets
   wadd(kSkCap * 4);                                  // batched-GEMV split-K partials
   wadd(kSkTickets * 4);                              // and their tickets
-  const bool gsk = s->bf16 && T > 32;                // prefill-capable bf16 stage: stream-K GEMM workspace
-  if (gsk) { wadd(kGskCap * 4); wadd(kGskTickets * 4); }
   s->wsbytes = woff;
   if (hipMalloc(&s->ws, s->wsbytes) != hipSuccess) return cleanup(fail(BS_ERR_OOM, "workspace allocation failed"));
   int wi = 0;
@@ -605,10 +597,6 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   s->att_tickets = (unsigned*)(s->ws + wo[wi++]);
   s->sk_ws = (float*)(s->ws + wo[wi++]);
   s->sk_tickets = (unsigned*)(s->ws + wo[wi++]);
-  if (gsk) {
-    s->gsk_ws = (float*)(s->ws + wo[wi++]);
-    s->gsk_tickets = (unsigned*)(s->ws + wo[wi++]);
-  }
   HIP_TRY(hipMemsetAsync(s->ws, 0, s->wsbytes, s->own));
   std::vector<float> sl(desc->n_head);
   alibi_slopes(desc->n_head, sl.data());
@@ -835,8 +823,6 @@ static double gemv_bytes(const bs_stage* s, int M, int N, int K, int out_bytes) 
 static Epi with_splitk(const bs_stage* s, const Epi& ep) {
   Epi e = ep;
   e.sk_ws = s->sk_ws; e.sk_tickets = s->sk_tickets; e.sk_cap = kSkCap; e.sk_ntickets = kSkTickets;
-  e.gsk_ws = s->gsk_ws; e.gsk_tickets = s->gsk_tickets; e.gsk_cap = s->gsk_ws ? kGskCap : 0;
-  e.gsk_ntickets = s->gsk_ws ? kGskTickets : 0;
   return e;
 }
 

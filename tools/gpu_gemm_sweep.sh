@@ -1,7 +1,12 @@
-# prefill GEMM tile sweep (BS_GEMM_TILE) on the bench workloads: 1b1 S=512 and 7b1 B=8 S=512
+# prefill GEMM variant sweep on the bench's prefill numbers (one run per arm):
+#   bash tools/gpu_gemm_sweep.sh NAME "ENV_1" "ENV_2" ... [-- bench args]
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-for t in 0 1 2 3 4; do
-  BS_GEMM_TILE=$t timeout -k 10 300 python -u bench.py --cpu-baseline 0 --no-pmc --steps 8 --warmup 2 > gpurun_out/gemm_tile_$t.log 2>&1 || exit $?
-  BS_GEMM_TILE=$t timeout -k 10 300 python -u bench.py --cpu-baseline 0 --no-pmc --steps 8 --warmup 2 --model bloom-7b1 --batch 8 > gpurun_out/gemm_tile_7b1_$t.log 2>&1 || exit $?
+name=$1; shift
+arms=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do arms+=("$1"); shift; done; [ "$1" = "--" ] && shift
+out=gpurun_out/sweep_$name.log; : > $out
+for arm in "${arms[@]}"; do
+  r=$(env $arm timeout -k 10 300 python -u bench.py --cpu-baseline 0 --no-pmc --steps 8 --warmup 2 "$@" 2>/dev/null | tail -1) || exit 1
+  v=$(echo "$r" | python -c 'import json,sys; d=json.loads(sys.stdin.read())["prefill"]; print("prefill %.3f ms  gemm %.1f TFLOP/s (%.3f of peak)" % (d["ms"], d.get("gemm_TFLOPs", 0), d.get("gemm_frac_of_peak", 0)))')
+  echo "[$arm] $* : $v" >> $out
 done
+cat $out
