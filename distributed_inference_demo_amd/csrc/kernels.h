@@ -64,6 +64,12 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
                       const void* beta, float eps, void* xn_scratch, const void* W, int M, int N, int K,
                       const Epi& ep, hipStream_t s);
 
+// The first stage's layer 0 at M <= 2 (bf16): word_embeddings[ids] -> word_embeddings_layernorm (fp32,
+// stored to x_out: the residual stream) -> LN_in -> weight GEMV, one kernel.  False: not launched.
+bool launch_linear_emb(const int* ids, const void* wemb, const void* emb_g, const void* emb_b, float* x_out,
+                       const void* gamma, const void* beta, float eps, const void* W, int M, int N, int K,
+                       const Epi& ep, hipStream_t s);
+
 // Attention over the KV cache for B rows x S new queries per row (causal, ALiBi).
 struct AttnArgs {
   const void* q;       // T [B*S][hidden]
@@ -101,15 +107,18 @@ void launch_linear_parts(const AttnParts& p, const void* W, int M, int N, int K,
 
 // keys -> token ids
 // Reduce the per-tile keys of each row (and keys_in[m] if given) -> keys_out[m] / tokens[m] (either optional).
+// past_adv (optional): past_adv[m] += seq for every row (the decode step's last kernel advances the
+// device copy of the cached lengths; stage.hip skips set_past when the host's next step matches it).
 void launch_argmax_finalize(const unsigned long long* keys, int M, int ntiles, const unsigned long long* keys_in,
-                            unsigned long long* keys_out, int* tokens, hipStream_t s);
+                            unsigned long long* keys_out, int* tokens, hipStream_t s, int* past_adv = nullptr,
+                            int seq = 0);
 // past_dev[0..n) = values[0..n) (host), stream ordered, by kernel arguments (graph-capturable).
 // Seeded top-k sampling (include/bloomstage.h bs_set_sampling; decoding.cpp:24-66) of M rows from the
 // per-16-column tile keys (key_hi_index = 1) and the logits they came from ([M][ldl], column = vocab index).
 // Row b's draw is keyed by (seed, KV row slot + b, position past_dev[b] + seq).
 void launch_topk_sample(const unsigned long long* keys, int ntiles, const float* logits, int ldl, int M, int k,
                         float inv_temp, uint64_t seed, int slot, const int* past_dev, int seq, int* tokens,
-                        hipStream_t s);
+                        hipStream_t s, int* past_adv = nullptr);
 void launch_set_past(int* past_dev, const int* values, int n, hipStream_t s);
 
 // ---- Weight-only int8 (bf16 stages with BS_FLAG_INT8_WEIGHTS; kernels.hip "Weight-only int8") ----

@@ -278,6 +278,14 @@ struct LnArgs {
   const bf16* gamma;
   const bf16* beta;
   float eps;
+  // X_EMB (gemv_rows_kernel, the first stage's layer 0): row m is word_embeddings[ids[m]] normalised by
+  // word_embeddings_layernorm (emb_g, emb_b) in fp32 -- the residual stream, stored by block 0 to x_out --
+  // and then by (gamma, beta) as X_LN.  `x` is unused.
+  const int* ids;
+  const bf16* wemb;
+  const bf16* emb_g;
+  const bf16* emb_b;
+  float* x_out;
 };
 
 // NT: non-temporal weight loads; PF: prefetch the next U weight steps before this step's MFMAs.
@@ -584,8 +592,127 @@ __device__ unsigned long long g_stamps[65536 * 4];
 
 // Activation prologue of gemv_rows_kernel: X read as given, LayerNorm of fp32 rows, or the merge
 // of split-attention partials (attn_merge.h); the last two stage bf16 rows in LDS.
-enum XMode : int { X_PLAIN = 0, X_LN = 1, X_PARTS = 2 };
+enum XMode : int { X_PLAIN = 0, X_LN = 1, X_PARTS = 2, X_EMB = 3 };
 constexpr int kPartsPre = 2;  // 4-column groups per thread whose partial loads go out before the weights
+
+// Two-pass LayerNorm statistics (mean, then centred squares) of M <= MM rows held by the first 256
+// threads (thread t: columns t*4 + i*1024, i < 4, below K); every thread of the block returns them.
+template <int MM>
+__device__ __forceinline__ void ln_stats_256(const float4 (&v)[MM][4], int K, float eps, float* scratch,
+                                             float (&mean)[MM], float (&rstd)[MM]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool active = threadIdx.x < 256;
+  const float invk = 1.0f / (float)K;
+#pragma unroll
+  for (int pass = 0; pass < 2; pass++) {
+#pragma unroll
+    for (int m = 0; m < MM; m++) {
+      float a = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if (active && (int)threadIdx.x * 4 + i * 1024 < K) {
+          if (pass == 0) a += (v[m][i].x + v[m][i].y) + (v[m][i].z + v[m][i].w);
+          else {
+            const float d0 = v[m][i].x - mean[m], d1 = v[m][i].y - mean[m], d2 = v[m][i].z - mean[m], d3 = v[m][i].w - mean[m];
+            a += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+          }
+        }
+      }
+      a = wave_sum(a);
+      if (lane == 0 && active) scratch[pass * 32 + w * 8 + m] = a;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MM; m++) {
+      const float t = ((scratch[pass * 32 + m] + scratch[pass * 32 + 8 + m]) +
+                       (scratch[pass * 32 + 16 + m] + scratch[pass * 32 + 24 + m])) * invk;
+      if (pass == 0) mean[m] = t;
+      else rstd[m] = 1.0f / sqrtf(t + eps);
+    }
+  }
+  __syncthreads();  // scratch is reused by the caller
+}
+
+__device__ __forceinline__ void bf16x4_to_f32(const uint2 raw, float4& o) {
+  o = make_float4(__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xFFFF0000u),
+                  __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xFFFF0000u));
+}
+
+// X_EMB, part 1 (before the weight stream is issued): the ids and both LayerNorms' gamma / beta.
+template <int MM>
+__device__ __forceinline__ void emb_rows_prefetch(const LnArgs& ln, int M, int K, int (&id)[MM], uint2 (&egb)[4][2],
+                                                  uint2 (&gb)[4][2]) {
+#pragma unroll
+  for (int m = 0; m < MM; m++) id[m] = ln.ids[min(m, M - 1)];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int k = min((int)threadIdx.x * 4 + i * 1024, K - 4);
+    egb[i][0] = *reinterpret_cast<const uint2*>(ln.emb_g + k);
+    egb[i][1] = *reinterpret_cast<const uint2*>(ln.emb_b + k);
+    gb[i][0] = *reinterpret_cast<const uint2*>(ln.gamma + k);
+    gb[i][1] = *reinterpret_cast<const uint2*>(ln.beta + k);
+  }
+}
+
+// Part 2: gather the embedding rows, word_embeddings_layernorm (fp32; block 0 stores it as the residual
+// stream), then the layer's LN_in to bf16 rows in LDS.  The row loads are issued behind the weight stream
+// (they need the ids), so this part waits for the block's first weight chunks too.
+template <int MM>
+__device__ __forceinline__ void emb_rows_finish(const LnArgs& ln, int M, int K, const int (&id)[MM],
+                                                const uint2 (&egb)[4][2], const uint2 (&gb)[4][2], bf16* xs,
+                                                float* scratch) {
+  float4 v[MM][4];
+#pragma unroll
+  for (int m = 0; m < MM; m++) {
+    const bf16* row = ln.wemb + (size_t)id[m] * K;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int k = min((int)threadIdx.x * 4 + i * 1024, K - 4);
+      bf16x4_to_f32(*reinterpret_cast<const uint2*>(row + k), v[m][i]);
+    }
+  }
+  float mean[MM], rstd[MM];
+  ln_stats_256<MM>(v, K, ln.eps, scratch, mean, rstd);
+  const bool active = threadIdx.x < 256;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    float4 g, b;
+    bf16x4_to_f32(egb[i][0], g);
+    bf16x4_to_f32(egb[i][1], b);
+    const int k = (int)threadIdx.x * 4 + i * 1024;
+#pragma unroll
+    for (int m = 0; m < MM; m++) {
+      v[m][i].x = (v[m][i].x - mean[m]) * rstd[m] * g.x + b.x;
+      v[m][i].y = (v[m][i].y - mean[m]) * rstd[m] * g.y + b.y;
+      v[m][i].z = (v[m][i].z - mean[m]) * rstd[m] * g.z + b.z;
+      v[m][i].w = (v[m][i].w - mean[m]) * rstd[m] * g.w + b.w;
+      if (blockIdx.x == 0 && active && k < K && m < M) *reinterpret_cast<float4*>(ln.x_out + (size_t)m * K + k) = v[m][i];
+    }
+  }
+  ln_stats_256<MM>(v, K, ln.eps, scratch, mean, rstd);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int k = (int)threadIdx.x * 4 + i * 1024;
+    if (active && k < K) {
+      float4 g, b;
+      bf16x4_to_f32(gb[i][0], g);
+      bf16x4_to_f32(gb[i][1], b);
+#pragma unroll
+      for (int m = 0; m < MM; m++) {
+        if (m < M) {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 o;
+          o[0] = (bf16)((v[m][i].x - mean[m]) * rstd[m] * g.x + b.x);
+          o[1] = (bf16)((v[m][i].y - mean[m]) * rstd[m] * g.y + b.y);
+          o[2] = (bf16)((v[m][i].z - mean[m]) * rstd[m] * g.z + b.z);
+          o[3] = (bf16)((v[m][i].w - mean[m]) * rstd[m] * g.w + b.w);
+          *reinterpret_cast<bf16x4*>(xs + (size_t)m * K + k) = o;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
 
 // FL: probe flags for tools/gemv_probe.hip (0 in the product): 1 = temporal (not non-temporal) weight loads,
 // 2 = no activation loads (x = 1), 4 = no epilogue (a store that never fires keeps the math).
@@ -616,6 +743,9 @@ __global__ __launch_bounds__(LB) void gemv_rows_kernel(const bf16* __restrict__ 
   if constexpr (LN) {
     if (threadIdx.x < 256) ln_rows_load<MM>(ln, M, K, xv, xc, gb);
   }
+  int eid[XM == X_EMB ? MM : 1];
+  uint2 egb[4][2];
+  if constexpr (XM == X_EMB) emb_rows_prefetch<MM>(ln, M, K, eid, egb, gb);
   const int kq = K >> 2, ngroups = M * kq;  // PARTS: 4-column groups of all rows
   PartsRegs pr[XM == X_PARTS ? kPartsPre : 1];
   auto pld1 = [](const float* p, size_t i) { return p[i]; };
@@ -638,6 +768,9 @@ __global__ __launch_bounds__(LB) void gemv_rows_kernel(const bf16* __restrict__ 
   int xstride;
   if constexpr (LN) {
     ln_rows_finish<MM>(ln, M, K, xv, xc, gb, xs, scratch);
+    xg = xs; xstride = K;
+  } else if constexpr (XM == X_EMB) {
+    emb_rows_finish<MM>(ln, M, K, eid, egb, gb, xs, scratch);
     xg = xs; xstride = K;
   } else if constexpr (XM == X_PARTS) {
     auto put = [&](int g, const PartsRegs& r) {
@@ -1382,21 +1515,48 @@ static void rows_geometry(int N, int K, int M, int r_default, int* R, int* waves
   *waves = std::max(4, std::min(16, (rows_cu + r - 1) / r));
 }
 
+// Geometry of a non-argmax rows GEMV: rows per wave R, waves per block, 512-column chunks in flight U.
+static void rows_plan(int XM, int M, int N, int K, int* R, int* waves, int* U) {
+  const bool LN = XM == X_LN || XM == X_EMB;
+  // rows per wave (tools/gemv_probe.hip, profiles/r01_gemv_probe.log): 2 on short rows, else 1; LN
+  // variants 2-4 on wide N to amortise the per-block LayerNorm prologue
+  // LN-fused: >= 2 rows per wave halves the blocks that each redo the row's LayerNorm
+  // (profiles/r01_ln_rows_sweep.txt: 560m 1566 -> 1621 tok/s, 1b1 1229 -> 1242)
+  static const int plain_r = [] { const char* e = getenv("BS_PLAIN_R"); return e && *e ? atoi(e) : 0; }();  // sweeps
+  const int R0 = !LN ? (plain_r ? plain_r : (K <= 2048 ? 2 : 1)) : (N >= 12288 ? 4 : (N >= 2048 ? 2 : 1));
+  rows_geometry(N, K, M, R0, R, waves);
+  // U = 512-element chunks of a row in flight per iteration: an exact divisor of the row's chunk
+  // count, so every row streams in whole rounds with no re-loaded tail (K = 1536 -> 3, 6144 -> 12,
+  // 4096 -> 8, 16384 -> 8, 2560 -> 5, 1024 -> 2); fallback 4.
+  const int cpr = K / 512;
+  int u = (K % 512) ? 4 : (cpr <= 3 || cpr == 5 || cpr == 8 || cpr == 12) ? cpr
+        : (cpr % 12 == 0 ? 12 : (cpr % 8 == 0 ? 8 : (cpr % 5 == 0 ? 5 : 4)));
+  // wide blocks are bounded for 1024 threads (<= 128 VGPRs): keep the weight registers (R x U x 4 VGPRs)
+  // small enough that nothing spills (LayerNorm / merge prologues hold ~32 more); 8 KB
+  // per wave x up to 16 waves per CU is plenty in flight
+  if (*waves > 4) {
+    const int cap = (XM == X_PLAIN ? 12 : 8) / (M == 1 ? 1 : 2);  // measured spill-free (ISA metadata)
+    while (*R * u > cap) u = (u % 2 == 0) ? u / 2 : (u > 4 ? 4 : u - 1);
+  }
+  *U = u;
+}
+
 template <int XM>
 static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const AttnParts& pa, const bf16* w, int M, int N,
                                int K, const Epi& ep, hipStream_t s) {
-  constexpr bool LN = XM == X_LN;
   if (M > 4 || (K % 8) != 0 || K < 8 || (XM != X_PLAIN && K > 4096)) return false;
   // M = 3..4: rows loses to the MFMA GEMV on LN-fused and large shapes
   // (tools/gemv_bench.hip, profiles/r01_gemv_bench_m4.log); keep it for small plain GEMVs and the head
   // (and for PARTS, which only this kernel implements).
   if (XM == X_PLAIN && M > 2 && ep.kind != EPI_ARGMAX && (size_t)N * K > (size_t)16 << 20) return false;
-  if (XM == X_LN && M > 2 && ep.kind != EPI_ARGMAX) return false;
+  if ((XM == X_LN || XM == X_EMB) && M > 2 && ep.kind != EPI_ARGMAX) return false;
+  if (XM == X_EMB && (ep.kind == EPI_ARGMAX || (K % 4) != 0)) return false;
   // Tile choice from tools/gemv_bench.hip (profiles/r01_gemv_bench_m1_ur.log): U = 4 chunks of
   // every row in flight; the LN variants take 2-4 rows per wave on wide N to amortise the
   // per-block LayerNorm prologue; the head (argmax, 16 rows per block) keeps U = 2 on long K.
   if (ep.kind == EPI_ARGMAX) {  // a block = one 16-column tile
-    if (K <= 2048) {
+    if constexpr (XM == X_EMB) return false;
+    else if (K <= 2048) {
       if (M == 1) gemv_rows_launch<4, 1, XM, 4>(x, ln, pa, w, M, N, K, ep, s);
       else if (M == 2) gemv_rows_launch<4, 2, XM, 4>(x, ln, pa, w, M, N, K, ep, s);
       else gemv_rows_launch<4, 4, XM, 4>(x, ln, pa, w, M, N, K, ep, s);
@@ -1407,32 +1567,13 @@ static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const AttnParts&
     }
     return true;
   }
-  // rows per wave (tools/gemv_probe.hip, profiles/r01_gemv_probe.log): 2 on short rows, else 1; LN
-  // variants 2-4 on wide N to amortise the per-block LayerNorm prologue
-  // LN-fused: >= 2 rows per wave halves the blocks that each redo the row's LayerNorm
-  // (profiles/r01_ln_rows_sweep.txt: 560m 1566 -> 1621 tok/s, 1b1 1229 -> 1242)
-  static const int plain_r = [] { const char* e = getenv("BS_PLAIN_R"); return e && *e ? atoi(e) : 0; }();  // sweeps
-  const int R0 = !LN ? (plain_r ? plain_r : (K <= 2048 ? 2 : 1)) : (N >= 12288 ? 4 : (N >= 2048 ? 2 : 1));
-  int R, waves;
-  rows_geometry(N, K, M, R0, &R, &waves);
-  // U = 512-element chunks of a row in flight per iteration: an exact divisor of the row's chunk
-  // count, so every row streams in whole rounds with no re-loaded tail (K = 1536 -> 3, 6144 -> 12,
-  // 4096 -> 8, 16384 -> 8, 2560 -> 5, 1024 -> 2); fallback 4.
-  const int cpr = K / 512;
-  int U = (K % 512) ? 4 : (cpr <= 3 || cpr == 5 || cpr == 8 || cpr == 12) ? cpr
-        : (cpr % 12 == 0 ? 12 : (cpr % 8 == 0 ? 8 : (cpr % 5 == 0 ? 5 : 4)));
-  // wide blocks are bounded for 1024 threads (<= 128 VGPRs): keep the weight registers (R x U x 4 VGPRs)
-  // small enough that nothing spills (LayerNorm / merge prologues hold ~32 more); 8 KB per wave x up
-  // to 16 waves per CU is plenty in flight
-  if (waves > 4) {
-    const int cap = (XM == X_PLAIN ? 12 : 8) / (M == 1 ? 1 : 2);  // measured spill-free (ISA metadata)
-    while (R * U > cap) U = (U % 2 == 0) ? U / 2 : (U > 4 ? 4 : U - 1);
-  }
+  int R, waves, U;
+  rows_plan(XM, M, N, K, &R, &waves, &U);
   auto go = [&](auto rc, auto uc) {
     constexpr int RR = decltype(rc)::value, UU = decltype(uc)::value;
     if (M == 1) gemv_rows_launch<RR, 1, XM, UU>(x, ln, pa, w, M, N, K, ep, s, waves);
     else if (M == 2) gemv_rows_launch<RR, 2, XM, UU>(x, ln, pa, w, M, N, K, ep, s, waves);
-    else gemv_rows_launch<RR, 4, XM, UU>(x, ln, pa, w, M, N, K, ep, s, waves);
+    else if constexpr (XM != X_EMB) gemv_rows_launch<RR, 4, XM, UU>(x, ln, pa, w, M, N, K, ep, s, waves);
   };
   auto gu = [&](auto rc) {
     switch (U) {
@@ -1489,6 +1630,15 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
 bool linear_parts_supported(int M, int K, int head_dim, int nsplit) {
   return M >= 1 && M <= 4 && K % 8 == 0 && K >= 8 && K <= 4096 && head_dim % 4 == 0 && nsplit >= 2 &&
          nsplit <= kPartsMaxSplit;
+}
+
+bool launch_linear_emb(const int* ids, const void* wemb, const void* emb_g, const void* emb_b, float* x_out,
+                       const void* gamma, const void* beta, float eps, const void* W, int M, int N, int K,
+                       const Epi& ep, hipStream_t s) {
+  if (M < 1 || M > 2 || gemv_rows_disabled()) return false;
+  LnArgs ln{nullptr, 1, 0, (const bf16*)gamma, (const bf16*)beta, eps,
+            ids, (const bf16*)wemb, (const bf16*)emb_g, (const bf16*)emb_b, x_out};
+  return gemv_rows_dispatch<X_EMB>(nullptr, ln, AttnParts{}, (const bf16*)W, M, N, K, ep, s);
 }
 
 void launch_linear_parts(const AttnParts& p, const void* W, int M, int N, int K, const Epi& ep, hipStream_t s) {
@@ -2081,9 +2231,12 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------
+// past_adv (optional): row m's cached length advances by `seq` here, the step's last kernel (every
+// reader of past_dev ran before it in stream order), so back-to-back decode steps need no set_past launch.
 __global__ __launch_bounds__(1024) void argmax_finalize_kernel(const unsigned long long* keys, int ntiles,
                                                                 const unsigned long long* keys_in,
-                                                                unsigned long long* keys_out, int* tokens) {
+                                                                unsigned long long* keys_out, int* tokens,
+                                                                int* past_adv, int seq) {
   __shared__ unsigned long long sh[16];
   const int m = blockIdx.x;
   const unsigned long long* kr = keys + (size_t)m * ntiles;
@@ -2111,13 +2264,14 @@ __global__ __launch_bounds__(1024) void argmax_finalize_kernel(const unsigned lo
       if (keys_in) best = keys_in[m] > best ? keys_in[m] : best;
       if (keys_out) keys_out[m] = best;
       if (tokens) tokens[m] = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+      if (past_adv) past_adv[m] += seq;
     }
   }
 }
 
 void launch_argmax_finalize(const unsigned long long* keys, int M, int ntiles, const unsigned long long* keys_in,
-                            unsigned long long* keys_out, int* tokens, hipStream_t s) {
-  argmax_finalize_kernel<<<M, 1024, 0, s>>>(keys, ntiles, keys_in, keys_out, tokens);
+                            unsigned long long* keys_out, int* tokens, hipStream_t s, int* past_adv, int seq) {
+  argmax_finalize_kernel<<<M, 1024, 0, s>>>(keys, ntiles, keys_in, keys_out, tokens, past_adv, seq);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2163,8 +2317,8 @@ __device__ __forceinline__ uint32_t sample_bits(uint64_t seed, uint32_t row, uin
 __global__ __launch_bounds__(1024) void topk_sample_kernel(const unsigned long long* __restrict__ keys, int ntiles,
                                                            const float* __restrict__ logits, int ldl, int k,
                                                            float inv_temp, uint64_t seed, int slot,
-                                                           const int* __restrict__ past_dev, int seq,
-                                                           int* __restrict__ tokens) {
+                                                           const int* past_dev, int seq,
+                                                           int* __restrict__ tokens, int* past_adv) {
   __shared__ unsigned long long sh[17];
   __shared__ unsigned long long pick[16];
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -2226,13 +2380,16 @@ __global__ __launch_bounds__(1024) void topk_sample_kernel(const unsigned long l
       if (run > target) { sel = r; break; }
     }
     tokens[b] = pi[sel];
+    if (past_adv) past_adv[b] = pos;  // the only reader of past_dev[b] in this kernel is this thread
   }
 }
 
 void launch_topk_sample(const unsigned long long* keys, int ntiles, const float* logits, int ldl, int M, int k,
                         float inv_temp, uint64_t seed, int slot, const int* past_dev, int seq, int* tokens,
-                        hipStream_t s) {
-  if (M > 0) topk_sample_kernel<<<M, 1024, 0, s>>>(keys, ntiles, logits, ldl, k, inv_temp, seed, slot, past_dev, seq, tokens);
+                        hipStream_t s, int* past_adv) {
+  if (M > 0)
+    topk_sample_kernel<<<M, 1024, 0, s>>>(keys, ntiles, logits, ldl, k, inv_temp, seed, slot, past_dev, seq, tokens,
+                                          past_adv);
 }
 
 // Per-row cached positions, passed by value (graph-replayable: the kernels read the device copy).

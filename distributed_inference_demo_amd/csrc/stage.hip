@@ -115,6 +115,8 @@ struct bs_stage {
   int* ids = nullptr;                  // [T] staging for host ids
   int* past_dev = nullptr;
   unsigned* att_tickets = nullptr;     // [max_batch][n_head]
+  std::vector<int> past_next;          // what past_dev[0..B) holds after the enqueued forwards (last stage)
+  bool past_next_valid = false;
   float* sk_ws = nullptr;              // batched-GEMV split-K partials (kSkCap floats)
   unsigned* sk_tickets = nullptr;      // [kSkTickets]
   ProfClass prof;
@@ -900,6 +902,16 @@ static int logits_staging(bs_stage* s, size_t bytes, hipStream_t st, float** out
   return BS_OK;
 }
 
+// BS_EMB_FUSED=0: the embedding LayerNorm as its own kernel on the decode path (A/B switch).
+static bool emb_fusion_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("BS_EMB_FUSED");
+    on = !(e && *e == '0');
+  }
+  return on != 0;
+}
+
 // Enqueue one forward on `st`.  The kernels read each row's past_len from past_dev (device [B],
 // written ahead of the forward or of the graph replay); `pasts` is the host copy (profiling bytes).
 static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, void* out, float* logits, hipStream_t st,
@@ -915,13 +927,16 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
 
   // ---- input
   const float* cur = nullptr;
+  const int* ids = nullptr;
+  // bf16 decode of <= 2 rows: the embedding gather and its LayerNorm run in layer 0's LN + QKV kernel
+  const bool emb_fused = d.is_first && s->bf16 && !s->q8 && M <= 2 && s->L > 0 && emb_fusion_enabled();
   if (d.is_first) {
-    const int* ids = (const int*)in;
+    ids = (const int*)in;
     if (host_io) {
       HIP_TRY(hipMemcpyAsync(s->ids, ids, (size_t)M * 4, hipMemcpyHostToDevice, st));
       ids = s->ids;
     }
-    launch_layernorm(s->bf16, s->wemb, ids, 0, 0, s->emb_g, s->emb_b, s->xa, 1, M, h, d.ln_eps, st);
+    if (!emb_fused) launch_layernorm(s->bf16, s->wemb, ids, 0, 0, s->emb_g, s->emb_b, s->xa, 1, M, h, d.ln_eps, st);
     cur = s->xa;
   } else if (host_io) {
     HIP_TRY(hipMemcpyAsync(s->xa, in, (size_t)M * h * 4, hipMemcpyHostToDevice, st));
@@ -940,7 +955,14 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     e.kind = EPI_QKV; e.bias = w.t[T_QKV_B]; e.q_out = s->q; e.k_cache = kbase; e.v_cache = kbase + s->kv_half;
     e.hidden = h; e.head_dim = hd; e.max_ctx = d.max_ctx; e.n_head = nh; e.seq = S; e.slot = slot; e.past = past;
     e.past_dev = past_dev; e.ldo = 3 * h;
-    wlinear_ln(s, st, cur, w.t[T_LN1_G], w.t[T_LN1_B], w, T_QKV_W, M, 3 * h, h, with_splitk(s, e), 4);
+    bool done = false;
+    if (l == 0 && emb_fused) {
+      ProfScope p(s, st, 1, gemv_bytes(s, M, 3 * h, h, 4) + (double)M * h * (s->esz + 4));
+      done = launch_linear_emb(ids, s->wemb, s->emb_g, s->emb_b, s->xa, w.t[T_LN1_G], w.t[T_LN1_B], d.ln_eps,
+                               w.t[T_QKV_W], M, 3 * h, h, with_splitk(s, e), st);
+      if (!done) launch_layernorm(s->bf16, s->wemb, ids, 0, 0, s->emb_g, s->emb_b, s->xa, 1, M, h, d.ln_eps, st);
+    }
+    if (!done) wlinear_ln(s, st, cur, w.t[T_LN1_G], w.t[T_LN1_B], w, T_QKV_W, M, 3 * h, h, with_splitk(s, e), 4);
     // attention
     AttnArgs a{};
     a.q = s->q; a.k_cache = kbase; a.v_cache = kbase + s->kv_half; a.ctx_out = s->ctx; a.slopes = s->slopes;
@@ -992,11 +1014,12 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     if (sample && !e.logits) e.logits = s->sample_logits;
     linear_ln(s, st, cur, S, S - 1, s->lnf_g, s->lnf_b, s->wemb, B, V, h, with_splitk(s, e), 0);
     int* tok_out = host_io ? s->tok : (int*)out;
+    // the pick is the step's last kernel: it advances the device copy of every row's past_len by S
     if (sample)
       launch_topk_sample(s->keys, V / 16, e.logits, V, B, s->top_k, 1.0f / s->temperature, s->sample_seed, slot,
-                         past_dev, S, tok_out, st);
+                         past_dev, S, tok_out, st, s->past_dev);
     else
-      launch_argmax_finalize(s->keys, B, V / 16, nullptr, nullptr, tok_out, st);
+      launch_argmax_finalize(s->keys, B, V / 16, nullptr, nullptr, tok_out, st, s->past_dev, S);
     if (host_io) {
       HIP_TRY(hipMemcpyAsync(out, s->tok, (size_t)B * 4, hipMemcpyDeviceToHost, st));
       if (dev_logits) HIP_TRY(hipMemcpyAsync(logits, dev_logits, (size_t)B * V * 4, hipMemcpyDeviceToHost, st));
@@ -1095,7 +1118,11 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
   hipStream_t st = stream ? (hipStream_t)stream : s->own;
 
   // Decode steps on device buffers replay a captured hipGraph: the kernels read past_len from
-  // device memory, set by one small kernel ahead of the replay.
+  // device memory, set by one small kernel ahead of the replay -- unless the last forward (a last
+  // stage's, whose token pick advances past_dev by its seq) already left exactly these values there.
+  const bool past_matches = s->past_next_valid && (int)s->past_next.size() == B &&
+                            std::equal(pasts.begin(), pasts.end(), s->past_next.begin());
+  s->past_next_valid = false;  // until this forward is enqueued
   const bool graph = S == 1 && !host_io && s->prof.cls == 0 && graphs_enabled();
   if (graph) {
     GraphKey key{B, slot, step->flags, in, out, logits, st};
@@ -1118,15 +1145,20 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
       }
       s->graphs.push_back({key, exec});
     }
-    launch_set_past(s->past_dev, pasts.data(), B, st);
+    if (!past_matches) launch_set_past(s->past_dev, pasts.data(), B, st);
     HIP_TRY(hipGraphLaunch(exec, st));
   } else {
-    launch_set_past(s->past_dev, pasts.data(), B, st);
+    if (!past_matches) launch_set_past(s->past_dev, pasts.data(), B, st);
     int rc = enqueue_forward(s, step, in, out, logits, st, s->past_dev, pasts);
     if (rc != BS_OK) return rc;
   }
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(BS_ERR_DEVICE, std::string("kernel launch: ") + hipGetErrorString(err));
+  if (d.is_last) {  // the last kernel advanced past_dev[0..B) by S (stream-ordered before the next forward)
+    s->past_next.assign(pasts.begin(), pasts.end());
+    for (int& p : s->past_next) p += S;
+    s->past_next_valid = true;
+  }
   if (host_io) HIP_TRY(hipStreamSynchronize(st));
   return BS_OK;
 }
