@@ -10,6 +10,10 @@
 //  fp32 mode (parity):       gemm_f32    — exact-fp32 LDS-tiled GEMM.
 //  attention: split-ctx decode (partial + combine) and a per-query online-softmax kernel
 //  for S > 1; both causal + ALiBi over the contiguous per-stage KV cache.
+#include <array>
+#include <cstdio>
+#include <cstring>
+#include <vector>
 #include "common.h"
 #include "kernels.h"
 #include "attn_merge.h"
@@ -902,66 +906,85 @@ __device__ __forceinline__ void q8x16_to_bf16(const u32x4v raw, bf16x8& lo, bf16
   }
 }
 
-template <int T, int MT, int WAVES, typename WT = bf16>
+template <int T, int MT, int WAVES, typename WT = bf16, int PD = 2, bool IL = false, int J = 2>
 __global__ __launch_bounds__(WAVES * 64) void gemv_tiles_kernel(const WT* __restrict__ W, const bf16* __restrict__ X,
                                                                 int M, int N, int K, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int RS = MT * 16 + 1;  // padded LDS row: [n][m]
+  constexpr int KU = 32 * J;       // K columns per unit: J MFMA k-steps; lane g holds 8J contiguous columns
   float* red = reinterpret_cast<float*>(smem);  // [WAVES][T * 16][RS]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * (T * 16);
   // split-K: block (x, ks) takes units [ks * upb, (ks + 1) * upb), its waves split those
   const int KS = gridDim.y, ks = blockIdx.y;
-  const int units_all = K >> 6, upb = (units_all + KS - 1) / KS;
+  const int units_all = K / KU, upb = (units_all + KS - 1) / KS;
   const int ub0 = min(units_all, ks * upb), units = min(units_all, ub0 + upb) - ub0;
   const int per = (units + WAVES - 1) / WAVES;
   const int u0 = ub0 + min(units, w * per), u1 = ub0 + min(units, w * per + per);
   const WT* wp[T];
 #pragma unroll
-  for (int t = 0; t < T; t++) wp[t] = W + (size_t)min(n0 + t * 16 + r, N - 1) * K + g * 16;
+  for (int t = 0; t < T; t++) wp[t] = W + (size_t)min(n0 + t * 16 + r, N - 1) * K + g * 8 * J;
   const bf16* xp[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; mt++) xp[mt] = X + (size_t)min(mt * 16 + r, M - 1) * K + g * 16;
+  for (int mt = 0; mt < MT; mt++) xp[mt] = X + (size_t)min(mt * 16 + r, M - 1) * K + g * 8 * J;
   f32x4 acc[T][MT];
 #pragma unroll
   for (int t = 0; t < T; t++)
 #pragma unroll
     for (int mt = 0; mt < MT; mt++) acc[t][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  bf16x8 a[T][2], b[MT][2];
-  auto load = [&](int u, bf16x8 (&aa)[T][2], bf16x8 (&bb)[MT][2]) {
-    const size_t o = (size_t)u * 64;
+  // a unit's raw operands: per tile J bf16x8 (bf16) or J / 2 16-B int8 words (converted where used); k-step
+  // j of a unit takes columns 8j .. 8j + 8 of every lane's run, in A (weights) and B (activations) alike
+  constexpr bool Q8 = sizeof(WT) == 1;
+  constexpr int NW = Q8 ? J / 2 : J;
+  typedef u32x4v RawW[NW];
+  auto load = [&](int u, RawW (&aa)[T], bf16x8 (&bb)[MT][J]) {
+    const size_t o = (size_t)u * KU;
 #pragma unroll
-    for (int t = 0; t < T; t++) {
-      if constexpr (sizeof(WT) == 1) {
-        q8x16_to_bf16(__builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(wp[t] + o)), aa[t][0], aa[t][1]);
-      } else {
-        aa[t][0] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[t] + o));
-        aa[t][1] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[t] + o + 8));
-      }
-    }
+    for (int t = 0; t < T; t++)
 #pragma unroll
-    for (int mt = 0; mt < MT; mt++) {
-      bb[mt][0] = *reinterpret_cast<const bf16x8*>(xp[mt] + o);
-      bb[mt][1] = *reinterpret_cast<const bf16x8*>(xp[mt] + o + 8);
-    }
+      for (int h = 0; h < NW; h++)
+        aa[t][h] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(wp[t] + o + h * 16 / sizeof(WT)));
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+      for (int j = 0; j < J; j++) bb[mt][j] = *reinterpret_cast<const bf16x8*>(xp[mt] + o + 8 * j);
   };
-  if (u0 < u1) load(u0, a, b);
-  for (int u = u0; u < u1; u++) {
-    bf16x8 an[T][2], bn[MT][2];
-    const bool more = u + 1 < u1;
-    if (more) load(u + 1, an, bn);
+  // Register ring of PD units: slot p holds unit i + p of the wave's list; after its MFMAs the slot is
+  // refilled with unit i + p + PD.  The loads are unconditional (clamped: a re-read of the wave's last unit
+  // is unused) so the compiler counts them with vmcnt(N) and keeps PD - 1 units in flight behind the MFMAs.
+  // IL: wave w takes units w, w + WAVES, ... of its block's range (the CU's waves stream adjacent K
+  // columns of the same rows); otherwise a contiguous range per wave
+  const int nu = IL ? (units > w ? (units - w + WAVES - 1) / WAVES : 0) : u1 - u0;
+  auto unit = [&](int i) { return IL ? ub0 + w + min(i, nu - 1) * WAVES : u0 + min(i, nu - 1); };
+  if (nu > 0) {
+    RawW a[PD][T];
+    bf16x8 b[PD][MT][J];
 #pragma unroll
-    for (int j = 0; j < 2; j++)
+    for (int p = 0; p < PD; p++) load(unit(p), a[p], b[p]);
+    for (int i = 0; i < nu; i += PD) {
 #pragma unroll
-      for (int t = 0; t < T; t++)
+      for (int p = 0; p < PD; p++) {
+        if (i + p < nu) {  // wave-uniform
+          bf16x8 w8[T][J];
 #pragma unroll
-        for (int mt = 0; mt < MT; mt++) acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t][j], b[mt][j], acc[t][mt], 0, 0, 0);
-    if (more) {
+          for (int t = 0; t < T; t++) {
 #pragma unroll
-      for (int t = 0; t < T; t++) { a[t][0] = an[t][0]; a[t][1] = an[t][1]; }
+            for (int h = 0; h < NW; h++) {
+              if constexpr (Q8) q8x16_to_bf16(a[p][t][h], w8[t][2 * h], w8[t][2 * h + 1]);
+              else w8[t][h] = __builtin_bit_cast(bf16x8, a[p][t][h]);
+            }
+          }
 #pragma unroll
-      for (int mt = 0; mt < MT; mt++) { b[mt][0] = bn[mt][0]; b[mt][1] = bn[mt][1]; }
+          for (int j = 0; j < J; j++)
+#pragma unroll
+            for (int t = 0; t < T; t++)
+#pragma unroll
+              for (int mt = 0; mt < MT; mt++)
+                acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w8[t][j], b[p][mt][j], acc[t][mt], 0, 0, 0);
+        }
+        load(unit(i + p + PD), a[p], b[p]);
+      }
     }
   }
   // D[row = 4g + i (n)][col = r (m)]
@@ -1040,7 +1063,12 @@ template <int T, int MT, int WAVES, typename WT = bf16>
 static void gemv_tiles_launch(const bf16* X, const WT* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s) {
   const size_t shm = sizeof(float) * WAVES * (T * 16) * (MT * 16 + 1);
   const int blocks = (N + T * 16 - 1) / (T * 16);
-  gemv_tiles_kernel<T, MT, WAVES, WT><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+  const dim3 g(blocks, KS);
+  // interleaved units: +12 % on bloom-7b1 B = 32 decode (profiles/r02_tiles_sweep.txt); BS_TILES_IL=0: contiguous
+  // unit ranges per wave; deeper register rings (PD 3, 4) and 4-k-step units measured slower
+  static const bool il = [] { const char* e = getenv("BS_TILES_IL"); return !(e && *e == '0'); }();
+  if (il) gemv_tiles_kernel<T, MT, WAVES, WT, 2, true><<<g, WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+  else gemv_tiles_kernel<T, MT, WAVES, WT, 2, false><<<g, WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
 }
 
 // Shape choice: the BLOOM shapes take the fastest (tiles, K splits, waves) of the
@@ -1051,7 +1079,7 @@ struct TileCfg { int N, K, T1, KS1, W1, T2, KS2, W2; };  // (T, KS, waves) for M
 static const TileCfg kTileTable[] = {
   {4608, 1536, 2, 1, 8, 2, 1, 8},    {1536, 1536, 1, 1, 8, 1, 2, 8},   {6144, 1536, 2, 1, 8, 2, 1, 8},
   {1536, 6144, 2, 4, 8, 2, 4, 8},    {7680, 2560, 2, 1, 8, 2, 1, 8},   {2560, 2560, 1, 1, 8, 1, 1, 8},
-  {10240, 2560, 2, 4, 4, 2, 2, 8},   {2560, 10240, 2, 8, 4, 2, 8, 8},  {12288, 4096, 1, 1, 4, 4, 1, 8},
+  {10240, 2560, 2, 4, 4, 2, 2, 8},   {2560, 10240, 2, 8, 4, 2, 8, 8},  {12288, 4096, 1, 1, 4, 3, 1, 8},
   {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 4, 4, 8, 4, 4, 8},
 };
 
@@ -1064,6 +1092,20 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
     if (c.N == N && c.K == K) {
       T = M > 16 ? c.T2 : c.T1; KS = M > 16 ? c.KS2 : c.KS1; WV = M > 16 ? c.W2 : c.W1;
     }
+  // BS_TILES_CFG="N,K,T,KS,W/...": per-shape override for M > 16 (sweeps)
+  static const std::vector<std::array<int, 5>> ovr = [] {
+    std::vector<std::array<int, 5>> v;
+    const char* e = getenv("BS_TILES_CFG");
+    while (e && *e) {
+      std::array<int, 5> c{};
+      if (sscanf(e, "%d,%d,%d,%d,%d", &c[0], &c[1], &c[2], &c[3], &c[4]) == 5) v.push_back(c);
+      e = strchr(e, '/');
+      if (e) e++;
+    }
+    return v;
+  }();
+  for (const auto& c : ovr)
+    if (M > 16 && c[0] == N && c[1] == K) { T = c[2]; KS = c[3]; WV = c[4]; }
   const int blocks = (N + T * 16 - 1) / (T * 16);
   const bool sk_ok = ep.sk_ws && ep.sk_tickets && blocks <= ep.sk_ntickets;
   if (WV == 0) {  // not in the table
@@ -1083,6 +1125,7 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
     else go(tc, EpiKindC<8>{});
   };
   if (T == 4) gw(EpiKindC<4>{});
+  else if (T == 3) gw(EpiKindC<3>{});
   else if (T == 2) gw(EpiKindC<2>{});
   else gw(EpiKindC<1>{});
   return true;
