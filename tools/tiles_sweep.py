@@ -43,7 +43,7 @@ def main():
         for i, nm in enumerate(names):
             if "attn_decode" not in nm:
                 continue
-            seq = [j for j in range(i - 3, min(len(rows), i + 5)) if "gemv_tiles" in names[j]]
+            seq = [j for j in range(i - 3, min(len(rows), i + 5)) if ("gemv_tiles" in names[j] or "gemv_ldsw" in names[j])]
             before = [j for j in seq if j < i]
             after = [j for j in seq if j > i]
             if before and len(after) >= 3:
