@@ -1072,42 +1072,39 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_tiles_kernel(const WT* __rest
 }
 
 // ------------------------------------------------------------------------------------
-// gemv_ldsw: the batched-decode tile GEMV with the weight stream read as the rows GEMV reads it.  The
-// MFMA operand layout wants 16 rows x 64 B per load instruction, which streamed at ~4.2 TB/s in the tile
-// kernel (profiles/r02_tiles_sweep.txt); here every load instruction reads 512 contiguous bytes of each
-// of 2 rows, the wave writes its 16 rows x 256 columns (8 KB) to a private LDS stage (16-B chunks XOR-
-// swizzled by row: conflict-free writes and fragment reads) and reads the A fragments from there.  Wave
-// w owns tile w % T and the K-part w / T of the block's K range; the next stage's weights and
-// activations are in flight (registers) while the current one is computed.  bf16 weights only.
+// gemv_ldsw4: the batched-decode GEMV with the weight stream read as the rows GEMV reads it.  The MFMA
+// operand layout wants 16 rows x 64 B per load instruction, which streamed at ~4.2 TB/s in gemv_tiles
+// (profiles/r02_tiles_sweep.txt); here a load instruction reads one 128-B line of each of 8 rows, the wave
+// writes its stage (T*16 rows x 64 columns) to a private LDS region (16-B chunks XOR-swizzled by row) and
+// reads the A fragments from there.  Every wave covers all T tiles of its block and a K part (waves split
+// K, as in gemv_tiles), so one wave's activation fragments serve T weight tiles; the next stage's weights
+// and activations are in flight (registers) while the current stage is computed.  bf16 weights.
 // ------------------------------------------------------------------------------------
-template <int T, int KH, int MT, int KC>  // KC: K columns per stage (256 or 128)
-__global__ __launch_bounds__(T * KH * 64) void gemv_ldsw_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
+template <int T, int WAVES, int MT, int KC>
+__global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
                                                                int M, int N, int K, Epi ep) {
-  constexpr int WAVES = T * KH, CPR = KC / 8;  // 16-B chunks per row per stage
-  constexpr int RPI = 64 / CPR, NI = 16 / RPI;  // rows per load instruction, instructions per 16 rows
+  constexpr int CPR = KC / 8, RPI = 64 / CPR, ROWS = T * 16, NI = ROWS / RPI;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int t = w % T, h = w / T;
-  bf16* wl = reinterpret_cast<bf16*>(smem) + (size_t)w * 16 * KC;
-  float* red = reinterpret_cast<float*>(smem + (size_t)WAVES * 16 * KC * sizeof(bf16));
-  const int n0 = blockIdx.x * (T * 16);
+  bf16* wl = reinterpret_cast<bf16*>(smem) + (size_t)w * ROWS * KC;
+  float* red = reinterpret_cast<float*>(smem + (size_t)WAVES * ROWS * KC * sizeof(bf16));
+  const int n0 = blockIdx.x * ROWS;
   const int KS = gridDim.y, ks = blockIdx.y;
-  const int kw = K / (KS * KH);                  // host: a multiple of KC
-  const int kbeg = ks * (K / KS) + h * kw, nst = kw / KC;
-  // load instruction i covers rows RPI*i .. RPI*i + RPI - 1 of the tile, chunk lc of each
+  const int kw = K / (KS * WAVES);  // host: a multiple of KC
+  const int kbeg = ks * (K / KS) + w * kw, nst = kw / KC;
   const int lr = lane / CPR, lc = lane % CPR;
-  const bf16* wsrc = W + (size_t)min(n0 + t * 16 + lr, N - 1) * K + kbeg + lc * 8;
-  const size_t wstep = (size_t)RPI * K;          // RPI rows down
-  auto swz = [](int row, int chunk) { return row * KC + ((chunk ^ (row & 15)) << 3); };  // element offset
+  const int rows_ok = min(ROWS, N - n0);
+  const bf16* wsrc = W + (size_t)min(n0 + lr, N - 1) * K + kbeg + lc * 8;
+  const size_t wstep = (size_t)RPI * K;
+  auto swz = [](int row, int chunk) { return row * KC + ((chunk ^ (row & (CPR - 1))) << 3); };
   const bf16* xsrc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; mt++) xsrc[mt] = X + (size_t)min(mt * 16 + r, M - 1) * K + kbeg + g * 8;
   u32x4v wr[2][NI];
-  bf16x8 xr[2][MT][CPR / 4];
-  auto load = [&](int st, u32x4v (&ww)[NI], bf16x8 (&xx)[MT][CPR / 4]) {
+  bf16x8 xr[2][MT][KC / 32];
+  auto load = [&](int st, u32x4v (&ww)[NI], bf16x8 (&xx)[MT][KC / 32]) {
     const size_t o = (size_t)st * KC;
-    const int rows_ok = min(16, N - (n0 + t * 16));  // rows past N re-read row N-1 (unused)
 #pragma unroll
     for (int i = 0; i < NI; i++) {
       const bf16* src = (RPI * i + lr < rows_ok) ? wsrc + i * wstep : wsrc;
@@ -1116,27 +1113,26 @@ __global__ __launch_bounds__(T * KH * 64) void gemv_ldsw_kernel(const bf16* __re
 #pragma unroll
     for (int mt = 0; mt < MT; mt++)
 #pragma unroll
-      for (int j = 0; j < CPR / 4; j++) xx[mt][j] = *reinterpret_cast<const bf16x8*>(xsrc[mt] + o + 32 * j);
+      for (int j = 0; j < KC / 32; j++) xx[mt][j] = *reinterpret_cast<const bf16x8*>(xsrc[mt] + o + 32 * j);
   };
   f32x4 acc[T][MT];
 #pragma unroll
-  for (int tt = 0; tt < T; tt++)
+  for (int t = 0; t < T; t++)
 #pragma unroll
-    for (int mt = 0; mt < MT; mt++) acc[tt][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 a2[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; mt++) a2[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MT; mt++) acc[t][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   auto stage = [&](int b, int st) {
     if (st + 1 < nst) load(st + 1, wr[b ^ 1], xr[b ^ 1]);
 #pragma unroll
     for (int i = 0; i < NI; i++) *reinterpret_cast<u32x4v*>(&wl[swz(RPI * i + lr, lc)]) = wr[b][i];
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int j = 0; j < CPR / 4; j++) {  // k-step j: columns 32j .. 32j + 32 of the stage, lane g: 8g .. 8g + 8
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(&wl[swz(r, 4 * j + g)]);
+    for (int j = 0; j < KC / 32; j++)
 #pragma unroll
-      for (int mt = 0; mt < MT; mt++) a2[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, xr[b][mt][j], a2[mt], 0, 0, 0);
-    }
+      for (int t = 0; t < T; t++) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(&wl[swz(t * 16 + r, 4 * j + g)]);
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++) acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, xr[b][mt][j], acc[t][mt], 0, 0, 0);
+      }
     __builtin_amdgcn_wave_barrier();
   };
   if (nst > 0) {
@@ -1146,22 +1142,14 @@ __global__ __launch_bounds__(T * KH * 64) void gemv_ldsw_kernel(const bf16* __re
       if (st + 1 < nst) stage(1, st + 1);
     }
   }
-#pragma unroll
-  for (int tt = 0; tt < T; tt++)
-#pragma unroll
-    for (int mt = 0; mt < MT; mt++) acc[tt][mt] = tt == t ? a2[mt] : (f32x4){0.f, 0.f, 0.f, 0.f};
   tiles_epilogue<T, MT, WAVES>(acc, red, M, N, n0, ep);
 }
 
-// Can gemv_ldsw run this shape with KS block K-splits of KH wave K-parts each, KC columns per stage?
-static bool ldsw_ok(int K, int KS, int KH, int KC) { return K % (KS * KH * KC) == 0; }
-
-template <int T, int KH, int MT, int KC>
-static void gemv_ldsw_launch(const bf16* X, const bf16* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s) {
-  constexpr int WAVES = T * KH;
-  const size_t shm = (size_t)WAVES * 16 * KC * sizeof(bf16) + sizeof(float) * WAVES * (T * 16) * (MT * 16 + 1);
+template <int T, int WAVES, int MT, int KC>
+static void gemv_ldsw4_launch(const bf16* X, const bf16* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s) {
+  const size_t shm = (size_t)WAVES * T * 16 * KC * sizeof(bf16) + sizeof(float) * WAVES * (T * 16) * (MT * 16 + 1);
   const int blocks = (N + T * 16 - 1) / (T * 16);
-  gemv_ldsw_kernel<T, KH, MT, KC><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+  gemv_ldsw4_kernel<T, WAVES, MT, KC><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
 }
 
 template <int T, int MT, int WAVES, typename WT = bf16>
@@ -1221,22 +1209,21 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
   if (KS > 1 && (!sk_ok || (size_t)KS * M * N > ep.sk_cap)) KS = 1;  // no workspace: no split
   const bool two = M > 16;
   if constexpr (sizeof(WT) == 2) {
-    // M <= 16: the LDS-transposed kernel on the non-square shapes (bloom-7b1 B=16: qkv 29.0 -> 27.0 us,
-    // fc1 33.0 -> 29.0, fc2 37.2 -> 31.3; the square dense projection stays faster on gemv_tiles, 12.1 vs
-    // 13.8 us; profiles/r02_tiles_sweep.txt).  M > 16: its per-wave activation reads (one tile per wave)
-    // outweigh the gain.  BS_TILES_LDSW=0: never, 2: every shape (A/B switches).
-    static const int ldsw_env = [] { const char* e = getenv("BS_TILES_LDSW"); return e && *e ? atoi(e) : 1; }();
-    const bool ldsw = ldsw_env == 2 || (ldsw_env == 1 && !two && N != K);
-    if (ldsw) {
-      // 64 rows per block; block K-splits until ~256 blocks (workspace permitting)
-      const int lb = (N + 63) / 64, kc = two ? 128 : 256;
-      int lks = 1;
-      while (lb * lks < 192 && sk_ok && (size_t)lks * 2 * M * N <= ep.sk_cap && ldsw_ok(K, lks * 2, 2, kc)) lks *= 2;
-      if (ldsw_ok(K, lks, 2, kc) && (lks == 1 || sk_ok)) {
-        if (two) gemv_ldsw_launch<4, 2, 2, 128>(x, w, M, N, K, lks, ep, s);
-        else gemv_ldsw_launch<4, 2, 1, 256>(x, w, M, N, K, lks, ep, s);
-        return true;
-      }
+    // gemv_ldsw4 at the table's (T, KS) (bloom-7b1 B=32: qkv 29.7 -> 21.3 us, dense 15.8 -> 12.5, fc1
+    // 36.4 -> 25.6, fc2 43.1 -> 32.0; decode steps: 7b1 B=16 +11 %, 3b B=8 +35 %, 1b1 B=8 +32 % over
+    // gemv_tiles; profiles/r02_tiles_sweep.txt).  BS_TILES_LDSW4=0: gemv_tiles only (A/B switch).
+    static const bool l4 = [] { const char* e = getenv("BS_TILES_LDSW4"); return !(e && *e == '0'); }();
+    if (l4 && T <= 4 && K % (KS * 8 * 64) == 0) {
+      auto go4 = [&](auto tc) {
+        constexpr int TT = decltype(tc)::value;
+        if (two) gemv_ldsw4_launch<TT, 8, 2, 64>(x, w, M, N, K, KS, ep, s);
+        else gemv_ldsw4_launch<TT, 8, 1, 64>(x, w, M, N, K, KS, ep, s);
+      };
+      if (T == 4) go4(EpiKindC<4>{});
+      else if (T == 3) go4(EpiKindC<3>{});
+      else if (T == 2) go4(EpiKindC<2>{});
+      else go4(EpiKindC<1>{});
+      return true;
     }
   }
   auto go = [&](auto tc, auto wc) {
