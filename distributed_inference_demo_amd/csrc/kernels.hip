@@ -1080,40 +1080,56 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_tiles_kernel(const WT* __rest
 // K, as in gemv_tiles), so one wave's activation fragments serve T weight tiles; the next stage's weights
 // and activations are in flight (registers) while the current stage is computed.  bf16 weights.
 // ------------------------------------------------------------------------------------
-template <int T, int WAVES, int MT, int KC>
-__global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
+// 8 int8 weights (8 bytes) -> bf16x8 exactly (|q| <= 127): u = q ^ 0x80 through v_cvt_f32_ubyte*, minus 128
+__device__ __forceinline__ bf16x8 q8x8_to_bf16(const uint2 raw) {
+  const uint32_t a = raw.x ^ 0x80808080u, b = raw.y ^ 0x80808080u;
+  bf16x8 o;
+  o[0] = (bf16)((float)(a & 0xFF) - 128.f); o[1] = (bf16)((float)((a >> 8) & 0xFF) - 128.f);
+  o[2] = (bf16)((float)((a >> 16) & 0xFF) - 128.f); o[3] = (bf16)((float)(a >> 24) - 128.f);
+  o[4] = (bf16)((float)(b & 0xFF) - 128.f); o[5] = (bf16)((float)((b >> 8) & 0xFF) - 128.f);
+  o[6] = (bf16)((float)((b >> 16) & 0xFF) - 128.f); o[7] = (bf16)((float)(b >> 24) - 128.f);
+  return o;
+}
+
+// WT = bf16 (KC = 64 columns = 128 B per row per stage) or int8_t (KC = 128 columns = 128 B; each A fragment
+// is 8 bytes converted in registers, the row scale applied by the epilogue's col_scale).
+template <int T, int WAVES, int MT, typename WT = bf16>
+__global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __restrict__ W, const bf16* __restrict__ X,
                                                                int M, int N, int K, Epi ep) {
-  constexpr int CPR = KC / 8, RPI = 64 / CPR, ROWS = T * 16, NI = ROWS / RPI;
+  constexpr int RB = 128, KC = RB / (int)sizeof(WT);  // bytes / columns of one row per stage
+  constexpr int CPR = RB / 16, RPI = 64 / CPR, ROWS = T * 16, NI = ROWS / RPI, KSTEP = KC / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  bf16* wl = reinterpret_cast<bf16*>(smem) + (size_t)w * ROWS * KC;
-  float* red = reinterpret_cast<float*>(smem + (size_t)WAVES * ROWS * KC * sizeof(bf16));
+  char* wl = smem + (size_t)w * ROWS * RB;
+  float* red = reinterpret_cast<float*>(smem + (size_t)WAVES * ROWS * RB);
   const int n0 = blockIdx.x * ROWS;
   const int KS = gridDim.y, ks = blockIdx.y;
   const int kw = K / (KS * WAVES);  // host: a multiple of KC
   const int kbeg = ks * (K / KS) + w * kw, nst = kw / KC;
   const int lr = lane / CPR, lc = lane % CPR;
   const int rows_ok = min(ROWS, N - n0);
-  const bf16* wsrc = W + (size_t)min(n0 + lr, N - 1) * K + kbeg + lc * 8;
+  const WT* wsrc = W + (size_t)min(n0 + lr, N - 1) * K + kbeg + lc * (16 / (int)sizeof(WT));
   const size_t wstep = (size_t)RPI * K;
-  auto swz = [](int row, int chunk) { return row * KC + ((chunk ^ (row & (CPR - 1))) << 3); };
+  auto swz = [](int row, int byte) {  // 16-B chunks XOR-swizzled by row
+    return row * RB + ((((byte >> 4) ^ (row & (CPR - 1)))) << 4) + (byte & 15);
+  };
   const bf16* xsrc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; mt++) xsrc[mt] = X + (size_t)min(mt * 16 + r, M - 1) * K + kbeg + g * 8;
   u32x4v wr[2][NI];
-  bf16x8 xr[2][MT][KC / 32];
-  auto load = [&](int st, u32x4v (&ww)[NI], bf16x8 (&xx)[MT][KC / 32]) {
+  bf16x8 xr[2][MT][KSTEP];
+  auto load = [&](int st, u32x4v (&ww)[NI], bf16x8 (&xx)[MT][KSTEP]) {
     const size_t o = (size_t)st * KC;
 #pragma unroll
     for (int i = 0; i < NI; i++) {
-      const bf16* src = (RPI * i + lr < rows_ok) ? wsrc + i * wstep : wsrc;
+      const WT* src = (RPI * i + lr < rows_ok) ? wsrc + i * wstep : wsrc;
       ww[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(src + o));
     }
 #pragma unroll
     for (int mt = 0; mt < MT; mt++)
 #pragma unroll
-      for (int j = 0; j < KC / 32; j++) xx[mt][j] = *reinterpret_cast<const bf16x8*>(xsrc[mt] + o + 32 * j);
+      for (int j = 0; j < KSTEP; j++) xx[mt][j] = *reinterpret_cast<const bf16x8*>(xsrc[mt] + o + 32 * j);
   };
   f32x4 acc[T][MT];
 #pragma unroll
@@ -1123,13 +1139,16 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const bf16* __re
   auto stage = [&](int b, int st) {
     if (st + 1 < nst) load(st + 1, wr[b ^ 1], xr[b ^ 1]);
 #pragma unroll
-    for (int i = 0; i < NI; i++) *reinterpret_cast<u32x4v*>(&wl[swz(RPI * i + lr, lc)]) = wr[b][i];
+    for (int i = 0; i < NI; i++) *reinterpret_cast<u32x4v*>(&wl[swz(RPI * i + lr, lc * 16)]) = wr[b][i];
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int j = 0; j < KC / 32; j++)
+    for (int j = 0; j < KSTEP; j++)
 #pragma unroll
       for (int t = 0; t < T; t++) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(&wl[swz(t * 16 + r, 4 * j + g)]);
+        // k-step j: columns 32j .. 32j + 32 of the stage; lane g takes 8g .. 8g + 8
+        bf16x8 af;
+        if constexpr (sizeof(WT) == 1) af = q8x8_to_bf16(*reinterpret_cast<const uint2*>(&wl[swz(t * 16 + r, 32 * j + 8 * g)]));
+        else af = *reinterpret_cast<const bf16x8*>(&wl[swz(t * 16 + r, 64 * j + 16 * g)]);
 #pragma unroll
         for (int mt = 0; mt < MT; mt++) acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, xr[b][mt][j], acc[t][mt], 0, 0, 0);
       }
@@ -1145,11 +1164,11 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const bf16* __re
   tiles_epilogue<T, MT, WAVES>(acc, red, M, N, n0, ep);
 }
 
-template <int T, int WAVES, int MT, int KC>
-static void gemv_ldsw4_launch(const bf16* X, const bf16* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s) {
-  const size_t shm = (size_t)WAVES * T * 16 * KC * sizeof(bf16) + sizeof(float) * WAVES * (T * 16) * (MT * 16 + 1);
+template <int T, int WAVES, int MT, typename WT>
+static void gemv_ldsw4_launch(const bf16* X, const WT* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s) {
+  const size_t shm = (size_t)WAVES * T * 16 * 128 + sizeof(float) * WAVES * (T * 16) * (MT * 16 + 1);
   const int blocks = (N + T * 16 - 1) / (T * 16);
-  gemv_ldsw4_kernel<T, WAVES, MT, KC><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+  gemv_ldsw4_kernel<T, WAVES, MT, WT><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
 }
 
 template <int T, int MT, int WAVES, typename WT = bf16>
@@ -1208,16 +1227,18 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
   }
   if (KS > 1 && (!sk_ok || (size_t)KS * M * N > ep.sk_cap)) KS = 1;  // no workspace: no split
   const bool two = M > 16;
-  if constexpr (sizeof(WT) == 2) {
+  {
     // gemv_ldsw4 at the table's (T, KS) (bloom-7b1 B=32: qkv 29.7 -> 21.3 us, dense 15.8 -> 12.5, fc1
     // 36.4 -> 25.6, fc2 43.1 -> 32.0; decode steps: 7b1 B=16 +11 %, 3b B=8 +35 %, 1b1 B=8 +32 % over
     // gemv_tiles; profiles/r02_tiles_sweep.txt).  BS_TILES_LDSW4=0: gemv_tiles only (A/B switch).
     static const bool l4 = [] { const char* e = getenv("BS_TILES_LDSW4"); return !(e && *e == '0'); }();
-    if (l4 && T <= 4 && K % (KS * 8 * 64) == 0) {
+    static const bool l4q = [] { const char* e = getenv("BS_TILES_LDSW4_Q8"); return !(e && *e == '0'); }();
+    constexpr int KC = 128 / (int)sizeof(WT);
+    if (l4 && (sizeof(WT) == 2 || l4q) && T <= 4 && K % (KS * 8 * KC) == 0) {
       auto go4 = [&](auto tc) {
         constexpr int TT = decltype(tc)::value;
-        if (two) gemv_ldsw4_launch<TT, 8, 2, 64>(x, w, M, N, K, KS, ep, s);
-        else gemv_ldsw4_launch<TT, 8, 1, 64>(x, w, M, N, K, KS, ep, s);
+        if (two) gemv_ldsw4_launch<TT, 8, 2, WT>(x, w, M, N, K, KS, ep, s);
+        else gemv_ldsw4_launch<TT, 8, 1, WT>(x, w, M, N, K, KS, ep, s);
       };
       if (T == 4) go4(EpiKindC<4>{});
       else if (T == 3) go4(EpiKindC<3>{});
