@@ -1192,7 +1192,7 @@ static const TileCfg kTileTable[] = {
   {4608, 1536, 2, 1, 8, 2, 1, 8},    {1536, 1536, 1, 1, 8, 1, 2, 8},   {6144, 1536, 2, 1, 8, 2, 1, 8},
   {1536, 6144, 2, 4, 8, 2, 4, 8},    {7680, 2560, 2, 1, 8, 2, 1, 8},   {2560, 2560, 1, 1, 8, 1, 1, 8},
   {10240, 2560, 2, 4, 4, 2, 2, 8},   {2560, 10240, 2, 8, 4, 2, 8, 8},  {12288, 4096, 1, 1, 4, 3, 1, 8},
-  {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 4, 4, 8, 4, 4, 8},
+  {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 4, 4, 8, 2, 2, 8},
 };
 
 template <typename WT = bf16>

@@ -1,11 +1,12 @@
-"""A/B numerics of a decode-path switch on the full bloom-1b1 stage (GPU), against the bf16 checker.
+"""A/B numerics of a decode-path env switch on the full bloom-1b1 stage (GPU), against the bf16 checker.
 
-    BS_ATTN_DENSE=1 python tools/diag_fused.py gpurun_out/fused.npz
-    BS_ATTN_DENSE=0 python tools/diag_fused.py gpurun_out/split.npz
-    python tools/diag_fused.py --compare gpurun_out/fused.npz gpurun_out/split.npz
+    SWITCH=1 python tools/diag_fused.py gpurun_out/a.npz
+    SWITCH=0 python tools/diag_fused.py gpurun_out/b.npz
+    python tools/diag_fused.py --compare gpurun_out/a.npz gpurun_out/b.npz
 
 Runs a 512-token prefill and 16 teacher-forced decode steps (the checker's tokens) and saves the GPU
-logits and the checker's logits per step.
+logits and the checker's logits per step.  Used for profiles/r02_attn_dense_numerics.txt (the
+attention + dense fusion of round 2, BS_ATTN_DENSE, since removed from the library).
 """
 import os
 import sys
@@ -48,7 +49,7 @@ def run(path):
     G, O = np.array(G), np.array(O)
     np.savez(path, gpu=G, ref=O)
     err = np.abs(G - O).max(axis=1)
-    print(os.environ.get("BS_ATTN_DENSE", "default"), "max-abs vs checker per step:", " ".join("%.4f" % e for e in err))
+    print(os.path.basename(path), "max-abs vs checker per step:", " ".join("%.4f" % e for e in err))
     print("mean-abs per step:", " ".join("%.5f" % e for e in np.abs(G - O).mean(axis=1)))
 
 
