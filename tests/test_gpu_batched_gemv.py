@@ -1,0 +1,36 @@
+"""Batched decode (4 < B <= 32 rows) through gemv_ldsw4 (kernels.hip: the weight stream read one 128-B
+line per row per load and transposed through a per-wave LDS stage), bf16 and weight-only int8, against
+the bf16-mode checker (oracle/bloom_oracle.c).  h = 1024 and 4h = 4096 make every block matrix a
+multiple of the kernel's K parts (8 waves x 64 bf16 / 128 int8 columns), so all four GEMVs and the
+argmax head run on it; ragged row counts (not a multiple of 16) exercise the clamped activation rows,
+B > 16 the two-m-tile variant, and the N = h GEMVs its split-K (write-through partials + ticket).
+The stage's parity bounds are tests/test_gpu_parity.py's (logits 2e-2 max-abs, ids by the checker's
+top-2 margin); reference tail: inference.cpp:272-327."""
+import numpy as np
+import pytest
+
+from oracle import gen_np
+
+from test_gpu_int8 import pair8
+from test_gpu_parity import assert_ids_match, check_logits, pair
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B", [5, 13, 17, 29])
+@pytest.mark.parametrize("weights", ["bf16", "int8"])
+def test_ldsw4_batched_decode_ragged_rows(B, weights):
+    h, nh, L, V = 1024, 16, 2, 4096
+    mk = pair8 if weights == "int8" else (lambda *a, **k: pair(*a[:6], "bf16", *a[6:], **k))
+    gs, os_ = mk(h, nh, L, V, 0, L, seed=21, max_batch=B + 3, max_ctx=24, max_tokens=B * 4)
+    ids = gen_np.prompt_ids(17, B, 4, V).astype(np.int32)
+    gs.forward_host(ids, B, 4, slot=3, past_len=0)
+    to = os_.forward(ids, B, 4, slot=3, past_len=0)
+    for step in range(3):
+        tg, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=3, past_len=4 + step, want_logits=True)
+        to_n, lo = os_.forward(to.reshape(B, 1), B, 1, slot=3, past_len=4 + step, want_logits=True)
+        check_logits(lg, lo, "bf16", f"{weights} B={B} decode step {step}")
+        assert_ids_match(tg, to_n, lo, f"{weights} B={B} decode step {step}")
+        to = to_n
+    gs.close()
+    os_.close()
