@@ -132,6 +132,11 @@ bool linear_q8_gemv(int M, int K);
 // dequantized into w_scratch (bf16, N*K) and the bf16 GEMM runs on it.
 void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* w_scratch, int M, int N, int K,
                       const Epi& ep, hipStream_t s);
+// The int8 dense GEMV on ctx = merge(split-attention partials) (M <= 2): the int8 counterpart of
+// launch_linear_parts.
+bool linear_q8_parts_supported(int M, int K, int head_dim, int nsplit);
+void launch_linear_q8_parts(const AttnParts& p, const int8_t* Q, const float* scale, int M, int N, int K,
+                            const Epi& ep, hipStream_t s);
 // M <= 4, K <= 4096: LayerNorm(x rows) fused into the int8 GEMV prologue (rows normalised to LDS).
 bool linear_q8_ln_fused(int M, int K);
 void launch_linear_q8_ln(const float* x, int row_stride, int row_offset, const void* gamma, const void* beta,

@@ -2632,10 +2632,10 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // streams 16 int8 weights (16 B, non-temporal) of each of its rows -- half the bytes of the bf16
 // rows GEMV -- and reads the 16 matching bf16 activations of every row m (L2-resident).  fp32
 // FMAs, DPP wave reduction, the row scale applied once to the reduced sum, then the usual epilogue.
-template <int R, int MM, bool LN, int KIND, int CW, bool XL>
+template <int R, int MM, bool LN, int KIND, int CW, bool XL, int UQ, bool PARTS>
 __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const float* __restrict__ scale,
-                                             const bf16* __restrict__ Xg, const LnArgs& ln, int M, int N, int K,
-                                             const Epi& ep) {
+                                             const bf16* __restrict__ Xg, const LnArgs& ln, const AttnParts& pa,
+                                             int M, int N, int K, const Epi& ep) {
   // Offset form: u = q + 128 (one XOR per 4 weights) converts with v_cvt_f32_ubyte{0..3}, one op per
   // weight; sum_k x*q = sum_k x*u - 128 * sum_k x, the activation sum shared by the R rows.  The
   // FMAs run on float pairs (v_pk_fma_f32).
@@ -2653,17 +2653,32 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
   const int8_t* wr[R];
 #pragma unroll
   for (int r = 0; r < R; r++) wr[r] = Q + (size_t)min(n0 + r, N - 1) * K;
-  // CW bytes of each row per lane per step (16 or 32): the next step's R x CW bytes are in flight
-  // during this step's FMAs
+  // CW bytes of each row per lane per step (16 or 32); UQ steps of every row in flight (the whole row up
+  // to UQ * 64 * CW bytes: one round trip for a 1536- or 6144-column row, as the bf16 rows GEMV); the
+  // loads are unconditional (clamped to the row; a step past the end is not computed)
   constexpr int W = CW / 16, STEP = 64 * CW;
-  int c = lane * CW;
-  i32x4 wv[R][W];
-  if (c < K) {
+  const int c0 = lane * CW;
+  i32x4 wv[UQ][R][W];
+  auto issue = [&](int base) {
 #pragma unroll
-    for (int r = 0; r < R; r++)
+    for (int u = 0; u < UQ; u++) {
+      const int c = min(base + u * STEP, K - CW);
 #pragma unroll
-      for (int w = 0; w < W; w++) wv[r][w] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c + 16 * w));
+      for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int w = 0; w < W; w++) wv[u][r][w] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c + 16 * w));
+    }
+  };
+  // PARTS: the split-attention partials (attn_merge.h) go out before the weights
+  const int kq = K >> 2, ngroups = M * kq;
+  PartsRegs pr[PARTS ? 1 : 1];
+  auto pld1 = [](const float* p, size_t i) { return p[i]; };
+  auto pld4 = [](const float* p, size_t i) { return *reinterpret_cast<const float4*>(p + i); };
+  if constexpr (PARTS) {
+    const int g = min((int)threadIdx.x, ngroups - 1);
+    attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, pr[0]);
   }
+  issue(c0);
   // LN: the block normalises its M fp32 rows into LDS while the first weight loads fly
   extern __shared__ __align__(16) unsigned char q8_lds[];
   const bf16* X = Xg;
@@ -2675,6 +2690,25 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
     ln_rows_load<MM>(ln, M, K, xv, cc, gb);
     ln_rows_finish<MM>(ln, M, K, xv, cc, gb, reinterpret_cast<bf16*>(q8_lds), scratch);
     X = reinterpret_cast<const bf16*>(q8_lds);
+  } else if constexpr (PARTS) {  // merged context rows (bf16, the attn_decode_kernel rounding) to LDS
+    bf16* xl = reinterpret_cast<bf16*>(q8_lds);
+    auto put = [&](int g, const PartsRegs& rr) {
+      float o[4];
+      attn_parts_combine(pa.nsplit, rr, o);
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[j] = (bf16)o[j];
+      *reinterpret_cast<bf16x4*>(xl + (size_t)(g / kq) * K + (g % kq) * 4) = v;
+    };
+    if ((int)threadIdx.x < ngroups) put(threadIdx.x, pr[0]);
+    for (int g = threadIdx.x + 256; g < ngroups; g += 256) {
+      PartsRegs rr;
+      attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, rr);
+      put(g, rr);
+    }
+    __syncthreads();
+    X = xl;
   } else if (XL) {  // plain X staged once per block in LDS (the 4 waves share it; one L2 pass)
     const int n16 = M * K / 8;
     for (int i = threadIdx.x; i < n16; i += 256)
@@ -2682,49 +2716,51 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
     __syncthreads();
     X = reinterpret_cast<const bf16*>(q8_lds);
   }
-  for (; c < K; c += STEP) {
-    i32x4 cur[R][W];
+  for (int base = c0; base < K; base += UQ * STEP) {
+    const bool more = base + UQ * STEP < K;
 #pragma unroll
-    for (int r = 0; r < R; r++)
+    for (int u = 0; u < UQ; u++) {
+      if (base + u * STEP >= K) continue;
 #pragma unroll
-      for (int w = 0; w < W; w++) cur[r][w] = wv[r][w];
-    if (c + STEP < K) {
+      for (int w = 0; w < W; w++) {
+        const int cw = base + u * STEP + 16 * w;
+        i32x4 cur[R];
 #pragma unroll
-      for (int r = 0; r < R; r++)
-#pragma unroll
-        for (int w = 0; w < W; w++)
-          wv[r][w] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c + STEP + 16 * w));
-    }
-#pragma unroll
-    for (int w = 0; w < W; w++) {
-      const int cw = c + 16 * w;
-      f2 wf[R][8];
-#pragma unroll
-      for (int r = 0; r < R; r++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const uint32_t u = (uint32_t)cur[r][w][i] ^ 0x80808080u;
-          wf[r][2 * i] = f2{(float)(u & 0xFF), (float)((u >> 8) & 0xFF)};
-          wf[r][2 * i + 1] = f2{(float)((u >> 16) & 0xFF), (float)(u >> 24)};
-        }
-#pragma unroll
-      for (int m = 0; m < MM; m++) {
-        if (m < M) {
-          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-          const u32x4 a0 = *reinterpret_cast<const u32x4*>(X + (size_t)m * K + cw);
-          const u32x4 a1 = *reinterpret_cast<const u32x4*>(X + (size_t)m * K + cw + 8);
-          f2 xf[8];
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            xf[i] = f2{__uint_as_float(a0[i] << 16), __uint_as_float(a0[i] & 0xFFFF0000u)};
-            xf[4 + i] = f2{__uint_as_float(a1[i] << 16), __uint_as_float(a1[i] & 0xFFFF0000u)};
-          }
-#pragma unroll
-          for (int i = 0; i < 8; i++) xs[m] += xf[i];
+        for (int r = 0; r < R; r++) cur[r] = wv[u][r][w];
+        if (more) {  // step u of the next round replaces it in flight
+          const int c = min(base + (UQ + u) * STEP, K - CW);
 #pragma unroll
           for (int r = 0; r < R; r++)
+            wv[u][r][w] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr[r] + c + 16 * w));
+        }
+        f2 wf[R][8];
 #pragma unroll
-            for (int i = 0; i < 8; i++) acc[r][m] = __builtin_elementwise_fma(xf[i], wf[r][i], acc[r][m]);
+        for (int r = 0; r < R; r++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const uint32_t uq = (uint32_t)cur[r][i] ^ 0x80808080u;
+            wf[r][2 * i] = f2{(float)(uq & 0xFF), (float)((uq >> 8) & 0xFF)};
+            wf[r][2 * i + 1] = f2{(float)((uq >> 16) & 0xFF), (float)(uq >> 24)};
+          }
+#pragma unroll
+        for (int m = 0; m < MM; m++) {
+          if (m < M) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 a0 = *reinterpret_cast<const u32x4*>(X + (size_t)m * K + cw);
+            const u32x4 a1 = *reinterpret_cast<const u32x4*>(X + (size_t)m * K + cw + 8);
+            f2 xf[8];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              xf[i] = f2{__uint_as_float(a0[i] << 16), __uint_as_float(a0[i] & 0xFFFF0000u)};
+              xf[4 + i] = f2{__uint_as_float(a1[i] << 16), __uint_as_float(a1[i] & 0xFFFF0000u)};
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) xs[m] += xf[i];
+#pragma unroll
+            for (int r = 0; r < R; r++)
+#pragma unroll
+              for (int i = 0; i < 8; i++) acc[r][m] = __builtin_elementwise_fma(xf[i], wf[r][i], acc[r][m]);
+          }
         }
       }
     }
@@ -2743,12 +2779,13 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
   if (lane < R * MM && m < M && n0 + r < N) epi_store<bf16, KIND>(ep, m, n0 + r, mine);  // ep.col_scale = scale
 }
 
-template <int R, int MM, bool LN, int CW, bool XL = false>
+template <int R, int MM, bool LN, int CW, bool XL = false, int UQ = 2, bool PARTS = false>
 __global__ __launch_bounds__(256) void gemv_q8_kernel(const int8_t* __restrict__ Q, const float* __restrict__ scale,
-                                                      const bf16* __restrict__ X, LnArgs ln, int M, int N, int K, Epi ep) {
+                                                      const bf16* __restrict__ X, LnArgs ln, AttnParts pa, int M,
+                                                      int N, int K, Epi ep) {
   epi_dispatch(ep.kind, [&](auto kc) {
     if constexpr (decltype(kc)::value != EPI_ARGMAX)
-      gemv_q8_body<R, MM, LN, decltype(kc)::value, CW, XL>(Q, scale, X, ln, M, N, K, ep);
+      gemv_q8_body<R, MM, LN, decltype(kc)::value, CW, XL, UQ, PARTS>(Q, scale, X, ln, pa, M, N, K, ep);
   });
 }
 
@@ -2761,24 +2798,40 @@ static int q8_cw() {
   return v;
 }
 
-template <int R, int MM, bool LN = false>
+template <int R, int MM, bool LN = false, bool PARTS = false>
 static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, const LnArgs& ln, int M, int N, int K,
-                           const Epi& ep, hipStream_t s) {
+                           const Epi& ep, hipStream_t s, const AttnParts& pa = AttnParts{}) {
   static const bool xl = [] {  // BS_Q8_XL=1: plain X staged in LDS when it fits 64 KB (A/B knob)
     const char* e = getenv("BS_Q8_XL");
     return e && *e == '1';
   }();
-  const bool stage_x = !LN && xl && (size_t)M * K * sizeof(bf16) <= 65536;
-  const size_t shm = (LN || stage_x) ? (size_t)M * K * sizeof(bf16) : 0;
+  const bool stage_x = !LN && !PARTS && xl && (size_t)M * K * sizeof(bf16) <= 65536;
+  const size_t shm = (LN || PARTS || stage_x) ? (size_t)M * K * sizeof(bf16) : 0;
   const int blocks = (N + 4 * R - 1) / (4 * R);
-  if constexpr (!LN) {
+  // steps of every row in flight: the whole row (<= 8 steps of 64 x 16 B) for matrices up to 12 M weights,
+  // where the grid is a few waves per SIMD and latency decides (bloom-1b1 int8 B=1: 1207 -> 1221 tok/s);
+  // one step beyond, where the stream is bandwidth-bound and deeper queues only cost occupancy
+  // (bloom-7b1 int8: UQ=1 486.6, UQ=2 471.7, the whole row 454 tok/s; profiles/r02_q8_uq_ab.txt)
+  static const int uq_env = [] { const char* e = getenv("BS_Q8_UQ"); return e && *e ? atoi(e) : 0; }();  // A/B
+  const int steps = (K + 1023) / 1024;
+  const int uq = uq_env ? uq_env : (size_t)N * K > (12u << 20) ? 1 : min(steps <= 2 ? 2 : steps <= 4 ? 4 : steps <= 6 ? 6 : 8, R >= 4 ? 4 : 8);
+  if constexpr (!LN && !PARTS) {
     if (stage_x) {
-      gemv_q8_kernel<R, MM, false, 16, true><<<blocks, 256, shm, s>>>(Q, scale, X, ln, M, N, K, ep);
+      gemv_q8_kernel<R, MM, false, 16, true><<<blocks, 256, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
       return;
     }
   }
-  if (q8_cw() == 32) gemv_q8_kernel<R, MM, LN, 32><<<blocks, 256, shm, s>>>(Q, scale, X, ln, M, N, K, ep);
-  else gemv_q8_kernel<R, MM, LN, 16><<<blocks, 256, shm, s>>>(Q, scale, X, ln, M, N, K, ep);
+  if (uq == 1) {  // one step in flight
+    gemv_q8_kernel<R, MM, LN, 16, false, 1, PARTS><<<blocks, 256, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+  } else if (uq <= 2) {
+    gemv_q8_kernel<R, MM, LN, 16, false, 2, PARTS><<<blocks, 256, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+  } else if (uq <= 4) {
+    gemv_q8_kernel<R, MM, LN, 16, false, 4, PARTS><<<blocks, 256, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+  } else if (uq <= 6) {
+    gemv_q8_kernel<R, MM, LN, 16, false, 6, PARTS><<<blocks, 256, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+  } else {
+    gemv_q8_kernel<R, MM, LN, 16, false, 8, PARTS><<<blocks, 256, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+  }
 }
 
 bool linear_q8_gemv(int M, int K) { return M >= 1 && M <= 8 && K % 32 == 0; }
@@ -2811,6 +2864,19 @@ void launch_linear_q8_ln(const float* x, int row_stride, int row_offset, const v
           : gemv_q8_launch<1, 4, true>(Q, scale, nullptr, ln, M, N, K, e, s);
 }
 
+bool linear_q8_parts_supported(int M, int K, int head_dim, int nsplit) {
+  return M >= 1 && M <= 2 && K % 32 == 0 && K <= 4096 && head_dim % 4 == 0 && nsplit >= 2 && nsplit <= kPartsMaxSplit;
+}
+
+void launch_linear_q8_parts(const AttnParts& p, const int8_t* Q, const float* scale, int M, int N, int K,
+                            const Epi& ep, hipStream_t s) {
+  Epi e = ep;
+  e.col_scale = scale;
+  if (M <= 1 && q8_rows(N) == 4) gemv_q8_launch<4, 1, false, true>(Q, scale, nullptr, LnArgs{}, M, N, K, e, s, p);
+  else if (M <= 1) gemv_q8_launch<2, 1, false, true>(Q, scale, nullptr, LnArgs{}, M, N, K, e, s, p);
+  else gemv_q8_launch<2, 2, false, true>(Q, scale, nullptr, LnArgs{}, M, N, K, e, s, p);
+}
+
 void launch_quantize_rows(const void* W_bf16, int8_t* Q, float* scale, int N, int K, hipStream_t s) {
   if (N > 0) quantize_rows_kernel<<<N, 256, 0, s>>>((const bf16*)W_bf16, Q, scale, K);
 }
@@ -2838,6 +2904,9 @@ void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* 
   const bf16* x = (const bf16*)X;
   Epi e = ep;
   e.col_scale = scale;
+  // batched decode (4 < M <= 32): the int8 gemv_ldsw4 / tile GEMV converts in registers (no dequant pass);
+  // at M = 8 it reads the weights once where gemv_q8 re-reads activations per row (bloom-7b1 int8 B=8)
+  if (M > 4 && M <= 32 && !gemv_tiles_disabled() && gemv_tiles_dispatch<int8_t>(x, Q, M, N, K, e, s)) return;
   if (linear_q8_gemv(M, K)) {
     const int rr = q8_rows(N);
     const bool r2 = rr >= 2;
@@ -2849,8 +2918,6 @@ void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* 
     else gemv_q8_launch<1, 8>(Q, scale, x, ln, M, N, K, e, s);
     return;
   }
-  // batched decode (8 < M <= 32): the int8 tile GEMV converts in registers (no dequant pass)
-  if (!gemv_tiles_disabled() && gemv_tiles_dispatch<int8_t>(x, Q, M, N, K, e, s)) return;
   // prefill: dequantize to the bf16 scratch, then the bf16 GEMM
   launch_dequant_rows(Q, nullptr, w_scratch, N, K, s);
   launch_linear(1, X, w_scratch, M, N, K, e, s);

@@ -858,11 +858,21 @@ static double gemv_bytes_q8(const bs_stage* s, int M, int N, int K, int out_byte
 }
 
 // Block matrix t of a layer: int8 stages stream the int8 weights (launch_linear_q8).
+// BS_Q8_PARTS=0: the int8 stage's split decode attention merges in its own kernel (ticket) instead of
+// the int8 dense GEMV's prologue (A/B knob)
+static bool q8_parts_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("BS_Q8_PARTS");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 static void wlinear(bs_stage* s, hipStream_t st, const void* X, const Layer& w, int t, int M, int N, int K,
                     const Epi& ep, int out_bytes) {
   if (!w.sc[t]) {
     linear(s, st, X, w.t[t], M, N, K, ep, out_bytes);
-  } else if (linear_q8_gemv(M, K)) {
+  } else if (M <= 32) {  // int8 GEMV / batched tile GEMV: weight-stream bound
     ProfScope p(s, st, 1, gemv_bytes_q8(s, M, N, K, out_bytes));
     launch_linear_q8(X, (const int8_t*)w.t[t], w.sc[t], s->wtmp, M, N, K, ep, st);
   } else {
@@ -971,7 +981,9 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     a.max_chunks = s->max_chunks; a.chunk = s->chunk; a.tickets = s->att_tickets;
     // a split decode context merges in the dense GEMV's prologue when that kernel can take it
     const int nsplit = S == 1 ? attention_decode_splits(B, nh, s->max_chunks) : 1;
-    a.defer_merge = s->bf16 && !s->q8 && nsplit > 1 && linear_parts_supported(M, h, hd, nsplit);
+    a.defer_merge = s->bf16 && nsplit > 1 &&
+                    (w.sc[T_DENSE_W] ? q8_parts_enabled() && linear_q8_parts_supported(M, h, hd, nsplit)
+                                     : linear_parts_supported(M, h, hd, nsplit));
     {
       ProfScope p(s, st, 3, ctx_sum * nh * hd * 2 * s->esz);
       launch_attention(s->bf16, a, st);
@@ -981,8 +993,9 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     e2.kind = EPI_RESID; e2.bias = w.t[T_DENSE_B]; e2.out_f32 = s->attn; e2.resid = cur; e2.ldo = h;
     if (a.defer_merge) {
       const AttnParts parts{s->part_acc, s->part_ml, nsplit, nh, hd, s->max_chunks, slot};
-      ProfScope p(s, st, 1, gemv_bytes(s, M, h, h, 4));
-      launch_linear_parts(parts, w.t[T_DENSE_W], M, h, h, e2, st);
+      ProfScope p(s, st, 1, w.sc[T_DENSE_W] ? gemv_bytes_q8(s, M, h, h, 4) : gemv_bytes(s, M, h, h, 4));
+      if (w.sc[T_DENSE_W]) launch_linear_q8_parts(parts, (const int8_t*)w.t[T_DENSE_W], w.sc[T_DENSE_W], M, h, h, e2, st);
+      else launch_linear_parts(parts, w.t[T_DENSE_W], M, h, h, e2, st);
     } else {
       wlinear(s, st, s->ctx, w, T_DENSE_W, M, h, h, with_splitk(s, e2), 4);
     }
