@@ -2641,7 +2641,7 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
   // FMAs run on float pairs (v_pk_fma_f32).
   typedef float f2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
-  const int n0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;  // waves past N compute row N-1, store nothing
+  const int n0 = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * R;  // waves past N: row N-1, no store
   f2 acc[R][MM];
   f2 xs[MM];
 #pragma unroll
@@ -2687,7 +2687,7 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
     float4 xv[MM][4];
     float cc[MM];
     uint2 gb[4][2];
-    ln_rows_load<MM>(ln, M, K, xv, cc, gb);
+    if (threadIdx.x < 256) ln_rows_load<MM>(ln, M, K, xv, cc, gb);
     ln_rows_finish<MM>(ln, M, K, xv, cc, gb, reinterpret_cast<bf16*>(q8_lds), scratch);
     X = reinterpret_cast<const bf16*>(q8_lds);
   } else if constexpr (PARTS) {  // merged context rows (bf16, the attn_decode_kernel rounding) to LDS
@@ -2702,7 +2702,7 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
       *reinterpret_cast<bf16x4*>(xl + (size_t)(g / kq) * K + (g % kq) * 4) = v;
     };
     if ((int)threadIdx.x < ngroups) put(threadIdx.x, pr[0]);
-    for (int g = threadIdx.x + 256; g < ngroups; g += 256) {
+    for (int g = threadIdx.x + blockDim.x; g < ngroups; g += blockDim.x) {
       PartsRegs rr;
       attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, rr);
       put(g, rr);
@@ -2711,7 +2711,7 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
     X = xl;
   } else if (XL) {  // plain X staged once per block in LDS (the 4 waves share it; one L2 pass)
     const int n16 = M * K / 8;
-    for (int i = threadIdx.x; i < n16; i += 256)
+    for (int i = threadIdx.x; i < n16; i += blockDim.x)
       reinterpret_cast<u16x8*>(q8_lds)[i] = reinterpret_cast<const u16x8*>(Xg)[i];
     __syncthreads();
     X = reinterpret_cast<const bf16*>(q8_lds);
@@ -2779,8 +2779,11 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
   if (lane < R * MM && m < M && n0 + r < N) epi_store<bf16, KIND>(ep, m, n0 + r, mine);  // ep.col_scale = scale
 }
 
-template <int R, int MM, bool LN, int CW, bool XL = false, int UQ = 2, bool PARTS = false>
-__global__ __launch_bounds__(256) void gemv_q8_kernel(const int8_t* __restrict__ Q, const float* __restrict__ scale,
+// WIDE: one block of up to 16 waves per CU (the rows GEMV's per-CU geometry, rows_geometry): the
+// LayerNorm / merge prologue runs once per CU instead of once per 4 waves, and narrow N still spreads
+// over every CU.
+template <int R, int MM, bool LN, int CW, bool XL = false, int UQ = 2, bool PARTS = false, bool WIDE = false>
+__global__ __launch_bounds__(WIDE ? 1024 : 256) void gemv_q8_kernel(const int8_t* __restrict__ Q, const float* __restrict__ scale,
                                                       const bf16* __restrict__ X, LnArgs ln, AttnParts pa, int M,
                                                       int N, int K, Epi ep) {
   epi_dispatch(ep.kind, [&](auto kc) {
@@ -2818,6 +2821,27 @@ static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, c
   if constexpr (!LN && !PARTS) {
     if (stage_x) {
       gemv_q8_kernel<R, MM, false, 16, true><<<blocks, 256, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+      return;
+    }
+  }
+  static const bool wide_on = [] { const char* e = getenv("BS_Q8_WIDE"); return !(e && *e == '0'); }();  // A/B
+  if constexpr (MM == 1 && R <= 2) {
+    int rr = 0, waves = 0;
+    rows_geometry(N, K, M, R, &rr, &waves);
+    // matrices up to 32 M weights (bloom-1b1 int8 B=1 1206 -> 1281 tok/s, 560m 1685 -> 1768, 3b 735 -> 762;
+    // bloom-7b1's 50-67 M-weight QKV / fc1 / fc2 keep 4-wave blocks; profiles/r02_q8_uq_ab.txt)
+    if (wide_on && (size_t)N * K <= (32u << 20) && rr <= 2 && waves >= 4 && uq <= 6) {
+      auto go = [&](auto rc) {
+        constexpr int RW = decltype(rc)::value;
+        const int wb = (N + waves * RW - 1) / (waves * RW);
+        const dim3 g(wb), t(waves * 64);
+        if (uq == 1) gemv_q8_kernel<RW, 1, LN, 16, false, 1, PARTS, true><<<g, t, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+        else if (uq <= 2) gemv_q8_kernel<RW, 1, LN, 16, false, 2, PARTS, true><<<g, t, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+        else if (uq <= 4) gemv_q8_kernel<RW, 1, LN, 16, false, 4, PARTS, true><<<g, t, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+        else gemv_q8_kernel<RW, 1, LN, 16, false, 6, PARTS, true><<<g, t, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+      };
+      if (rr == 2) go(EpiKindC<2>{});
+      else go(EpiKindC<1>{});
       return;
     }
   }
