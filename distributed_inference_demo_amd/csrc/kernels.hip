@@ -1187,12 +1187,15 @@ static void gemv_tiles_launch(const bf16* X, const WT* W, int M, int N, int K, i
 // tools/gemv_probe.hip PROBE_SWEEP measurement (profiles/r01_gemv_sweep.log), per m-tile count;
 // other shapes: 2 tiles (4 from N >= 16384), K split until >= 192 blocks while each split keeps
 // >= 8 units, 8 waves when every wave gets >= 2 units.
+// bloom-3b fc1/fc2 and bloom-7b1 QKV/fc2 (M <= 16) re-swept for gemv_ldsw4 (whose K parts must divide
+// K: 3b fc1 had fallen back to gemv_tiles): 3b B=8 3031 -> 3927 tok/s, B=32 8124 -> 10624; 7b1 B=16 QKV
+// 21.2 -> 18.3 us, fc2 26.8 -> 24.6 us (profiles/r02_tiles_sweep.txt)
 struct TileCfg { int N, K, T1, KS1, W1, T2, KS2, W2; };  // (T, KS, waves) for M <= 16 and M <= 32
 static const TileCfg kTileTable[] = {
   {4608, 1536, 2, 1, 8, 2, 1, 8},    {1536, 1536, 1, 1, 8, 1, 2, 8},   {6144, 1536, 2, 1, 8, 2, 1, 8},
   {1536, 6144, 2, 4, 8, 2, 4, 8},    {7680, 2560, 2, 1, 8, 2, 1, 8},   {2560, 2560, 1, 1, 8, 1, 1, 8},
-  {10240, 2560, 2, 4, 4, 2, 2, 8},   {2560, 10240, 2, 8, 4, 2, 8, 8},  {12288, 4096, 1, 1, 4, 3, 1, 8},
-  {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 4, 4, 8, 2, 2, 8},
+  {10240, 2560, 3, 1, 8, 3, 1, 8},   {2560, 10240, 2, 2, 8, 2, 5, 8},  {12288, 4096, 3, 1, 8, 3, 1, 8},
+  {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 2, 2, 8, 2, 2, 8},
 };
 
 template <typename WT = bf16>
@@ -1204,10 +1207,9 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
     if (c.N == N && c.K == K) {
       T = M > 16 ? c.T2 : c.T1; KS = M > 16 ? c.KS2 : c.KS1; WV = M > 16 ? c.W2 : c.W1;
     }
-  // BS_TILES_CFG="N,K,T,KS,W/...": per-shape override for M > 16 (sweeps)
-  static const std::vector<std::array<int, 5>> ovr = [] {
+  // BS_TILES_CFG="N,K,T,KS,W/...": per-shape override for M > 16, BS_TILES_CFG1 for M <= 16 (sweeps)
+  auto parse = [](const char* e) {
     std::vector<std::array<int, 5>> v;
-    const char* e = getenv("BS_TILES_CFG");
     while (e && *e) {
       std::array<int, 5> c{};
       if (sscanf(e, "%d,%d,%d,%d,%d", &c[0], &c[1], &c[2], &c[3], &c[4]) == 5) v.push_back(c);
@@ -1215,9 +1217,11 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
       if (e) e++;
     }
     return v;
-  }();
-  for (const auto& c : ovr)
-    if (M > 16 && c[0] == N && c[1] == K) { T = c[2]; KS = c[3]; WV = c[4]; }
+  };
+  static const std::vector<std::array<int, 5>> ovr2 = parse(getenv("BS_TILES_CFG"));
+  static const std::vector<std::array<int, 5>> ovr1 = parse(getenv("BS_TILES_CFG1"));
+  for (const auto& c : (M > 16 ? ovr2 : ovr1))
+    if (c[0] == N && c[1] == K) { T = c[2]; KS = c[3]; WV = c[4]; }
   const int blocks = (N + T * 16 - 1) / (T * 16);
   const bool sk_ok = ep.sk_ws && ep.sk_tickets && blocks <= ep.sk_ntickets;
   if (WV == 0) {  // not in the table

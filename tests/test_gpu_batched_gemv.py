@@ -34,3 +34,22 @@ def test_ldsw4_batched_decode_ragged_rows(B, weights):
         to = to_n
     gs.close()
     os_.close()
+
+
+@pytest.mark.parametrize("B", [8, 20])
+def test_ldsw4_ragged_tile_columns(B):
+    """bloom-3b widths (h = 2560): fc1 (N = 10240) runs 3-tile blocks, so its last block is ragged
+    (10240 = 213 x 48 + 16), and fc2 (K = 10240) splits K in 2 (B <= 16) / 5 (B > 16) parts."""
+    h, nh, L, V = 2560, 32, 1, 4096
+    gs, os_ = pair(h, nh, L, V, 0, L, "bf16", seed=23, max_batch=B, max_ctx=16, max_tokens=B * 3)
+    ids = gen_np.prompt_ids(29, B, 3, V).astype(np.int32)
+    gs.forward_host(ids, B, 3, slot=0, past_len=0)
+    to = os_.forward(ids, B, 3, slot=0, past_len=0)
+    for step in range(2):
+        tg, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=0, past_len=3 + step, want_logits=True)
+        to_n, lo = os_.forward(to.reshape(B, 1), B, 1, slot=0, past_len=3 + step, want_logits=True)
+        check_logits(lg, lo, "bf16", f"h=2560 B={B} decode step {step}")
+        assert_ids_match(tg, to_n, lo, f"h=2560 B={B} decode step {step}")
+        to = to_n
+    gs.close()
+    os_.close()

@@ -26,7 +26,7 @@ def main():
         cfg = "/".join(f"{n},{k},{p}" for (name, n, k), p in zip(shapes, parts) if p)
         d = f"gpurun_out/tsw_{abs(hash(arm)) % 10**8}"
         shutil.rmtree(d, ignore_errors=True)
-        env = dict(os.environ, BS_TILES_CFG=cfg)
+        env = dict(os.environ, **{"BS_TILES_CFG" if batch > 16 else "BS_TILES_CFG1": cfg})
         cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", d, "-o",
                "run", "--", sys.executable, "bench.py", "--cpu-baseline", "0", "--no-pmc", "--no-profile", "--model",
                model, "--batch", str(batch), "--prompt", "128", "--steps", "24", "--warmup", "4"]
