@@ -1189,10 +1189,13 @@ static void gemv_tiles_launch(const bf16* X, const WT* W, int M, int N, int K, i
 // >= 8 units, 8 waves when every wave gets >= 2 units.
 // bloom-3b fc1/fc2 and bloom-7b1 QKV/fc2 (M <= 16) re-swept for gemv_ldsw4 (whose K parts must divide
 // K: 3b fc1 had fallen back to gemv_tiles): 3b B=8 3031 -> 3927 tok/s, B=32 8124 -> 10624; 7b1 B=16 QKV
-// 21.2 -> 18.3 us, fc2 26.8 -> 24.6 us (profiles/r02_tiles_sweep.txt)
+// 21.2 -> 18.3 us, fc2 26.8 -> 24.6 us; 1b1 dense at M > 16 (1, 1): 8.9 -> 6.8 us; 560m (h = 1024) rows added (B=32 QKV 8.1 -> 5.6 us;
+// profiles/r02_tiles_sweep.txt)
 struct TileCfg { int N, K, T1, KS1, W1, T2, KS2, W2; };  // (T, KS, waves) for M <= 16 and M <= 32
 static const TileCfg kTileTable[] = {
-  {4608, 1536, 2, 1, 8, 2, 1, 8},    {1536, 1536, 1, 1, 8, 1, 2, 8},   {6144, 1536, 2, 1, 8, 2, 1, 8},
+  {3072, 1024, 1, 1, 8, 1, 1, 8},    {1024, 1024, 1, 1, 8, 1, 1, 8},   {4096, 1024, 2, 1, 8, 2, 1, 8},
+  {1024, 4096, 1, 2, 8, 1, 4, 8},
+  {4608, 1536, 2, 1, 8, 2, 1, 8},    {1536, 1536, 1, 1, 8, 1, 1, 8},   {6144, 1536, 2, 1, 8, 2, 1, 8},
   {1536, 6144, 2, 4, 8, 2, 4, 8},    {7680, 2560, 2, 1, 8, 2, 1, 8},   {2560, 2560, 1, 1, 8, 1, 1, 8},
   {10240, 2560, 3, 1, 8, 3, 1, 8},   {2560, 10240, 2, 2, 8, 2, 5, 8},  {12288, 4096, 3, 1, 8, 3, 1, 8},
   {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 2, 2, 8, 2, 2, 8},
