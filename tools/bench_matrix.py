@@ -22,7 +22,8 @@ HBM_PEAK = 8000.0
 CONFIGS = [  # (model, batch, prompt, steps)
     ("bloom-560m", 1, 16, 128), ("bloom-1b1", 1, 512, 128), ("bloom-3b", 1, 64, 128), ("bloom-3b", 8, 64, 128),
     ("bloom-7b1", 1, 128, 128), ("bloom-7b1", 8, 512, 64), ("bloom-7b1", 32, 128, 64), ("bloom-7b1", 32, 1024, 32),
-    ("bloom-7b1", 32, 1984, 32),
+    ("bloom-7b1", 32, 1984, 32), ("bloom-7b1", 16, 128, 64), ("bloom-3b", 32, 64, 64), ("bloom-1b1", 8, 128, 64),
+    ("bloom-1b1", 32, 128, 64), ("bloom-560m", 16, 16, 128), ("bloom-560m", 32, 16, 128),
 ]
 
 
