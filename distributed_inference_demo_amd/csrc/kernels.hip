@@ -2685,16 +2685,20 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
     const int g = min((int)threadIdx.x, ngroups - 1);
     attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, pr[0]);
   }
+  // LN: the rows (and gamma/beta) go out before the weights -- loads return in order, so rows issued
+  // behind the weight stream would wait for all of it -- and the block normalises them into LDS while
+  // the weight loads fly
+  float4 xv[LN ? MM : 1][4];
+  float cc[LN ? MM : 1];
+  uint2 gb[4][2];
+  if constexpr (LN) {
+    if (threadIdx.x < 256) ln_rows_load<MM>(ln, M, K, xv, cc, gb);
+  }
   issue(c0);
-  // LN: the block normalises its M fp32 rows into LDS while the first weight loads fly
   extern __shared__ __align__(16) unsigned char q8_lds[];
   const bf16* X = Xg;
   if constexpr (LN) {
     __shared__ float scratch[64];
-    float4 xv[MM][4];
-    float cc[MM];
-    uint2 gb[4][2];
-    if (threadIdx.x < 256) ln_rows_load<MM>(ln, M, K, xv, cc, gb);
     ln_rows_finish<MM>(ln, M, K, xv, cc, gb, reinterpret_cast<bf16*>(q8_lds), scratch);
     X = reinterpret_cast<const bf16*>(q8_lds);
   } else if constexpr (PARTS) {  // merged context rows (bf16, the attn_decode_kernel rounding) to LDS
