@@ -2694,6 +2694,16 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
   if constexpr (LN) {
     if (threadIdx.x < 256) ln_rows_load<MM>(ln, M, K, xv, cc, gb);
   }
+  // XL: the plain X rows likewise go out ahead of the weights (up to 4 16-B pieces per thread)
+  constexpr int XP = XL ? 4 : 1;
+  u16x8 xpre[XP];
+  if constexpr (XL) {
+#pragma unroll
+    for (int j = 0; j < XP; j++) {
+      const int i = min((int)threadIdx.x + j * (int)blockDim.x, M * K / 8 - 1);
+      xpre[j] = reinterpret_cast<const u16x8*>(Xg)[i];
+    }
+  }
   issue(c0);
   extern __shared__ __align__(16) unsigned char q8_lds[];
   const bf16* X = Xg;
@@ -2720,9 +2730,14 @@ __device__ __forceinline__ void gemv_q8_body(const int8_t* __restrict__ Q, const
     }
     __syncthreads();
     X = xl;
-  } else if (XL) {  // plain X staged once per block in LDS (the 4 waves share it; one L2 pass)
+  } else if (XL) {  // plain X staged once per block in LDS (the block's waves share it; one L2 pass)
     const int n16 = M * K / 8;
-    for (int i = threadIdx.x; i < n16; i += blockDim.x)
+#pragma unroll
+    for (int j = 0; j < XP; j++) {
+      const int i = threadIdx.x + j * blockDim.x;
+      if (i < n16) reinterpret_cast<u16x8*>(q8_lds)[i] = xpre[j];
+    }
+    for (int i = threadIdx.x + XP * blockDim.x; i < n16; i += blockDim.x)
       reinterpret_cast<u16x8*>(q8_lds)[i] = reinterpret_cast<const u16x8*>(Xg)[i];
     __syncthreads();
     X = reinterpret_cast<const bf16*>(q8_lds);
@@ -2836,6 +2851,8 @@ static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, c
     }
   }
   static const bool wide_on = [] { const char* e = getenv("BS_Q8_WIDE"); return !(e && *e == '0'); }();  // A/B
+  static const bool wide_xl_on = [] { const char* e = getenv("BS_Q8_WIDE_XL"); return !(e && *e == '0'); }();  // A/B
+  const bool wide_xl = wide_xl_on && (size_t)M * K * sizeof(bf16) <= 65536;
   if constexpr (MM == 1 && R <= 2) {
     int rr = 0, waves = 0;
     rows_geometry(N, K, M, R, &rr, &waves);
@@ -2846,6 +2863,16 @@ static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, c
         constexpr int RW = decltype(rc)::value;
         const int wb = (N + waves * RW - 1) / (waves * RW);
         const dim3 g(wb), t(waves * 64);
+        if constexpr (!LN && !PARTS) {
+          if (wide_xl) {  // plain X staged in LDS, loaded ahead of the weights
+            const size_t shx = (size_t)M * K * sizeof(bf16);
+            if (uq == 1) gemv_q8_kernel<RW, 1, false, 16, true, 1, false, true><<<g, t, shx, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+            else if (uq <= 2) gemv_q8_kernel<RW, 1, false, 16, true, 2, false, true><<<g, t, shx, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+            else if (uq <= 4) gemv_q8_kernel<RW, 1, false, 16, true, 4, false, true><<<g, t, shx, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+            else gemv_q8_kernel<RW, 1, false, 16, true, 6, false, true><<<g, t, shx, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
+            return;
+          }
+        }
         if (uq == 1) gemv_q8_kernel<RW, 1, LN, 16, false, 1, PARTS, true><<<g, t, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
         else if (uq <= 2) gemv_q8_kernel<RW, 1, LN, 16, false, 2, PARTS, true><<<g, t, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
         else if (uq <= 4) gemv_q8_kernel<RW, 1, LN, 16, false, 4, PARTS, true><<<g, t, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
