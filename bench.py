@@ -39,6 +39,11 @@ def parse():
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     p.add_argument("--no-head-split", action="store_true", help="pipeline: keep the whole lm_head on the last stage")
+    p.add_argument("--pipeline", action="store_true",
+                   help="N = 1: report the pipeline code's line (weak + strong) instead of the single-stage one")
+    p.add_argument("--no-pipeline-n1", action="store_true",
+                   help="N = 1: skip the pipeline code's N = 1 point (the reference point of the N > 1 curve)")
+    p.add_argument("--no-strong", action="store_true", help="pipeline: skip the fixed-rows (strong) measurement")
     return p.parse_args()
 
 
@@ -59,7 +64,7 @@ def pmc_traffic(args, kernel_tag, timeout=240):
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         cmd = [prof, "--pmc", counter, "-d", out, "-o", counter.lower(), "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--steps", "8", "--warmup", "2", "--cpu-baseline", "0",
-               "--no-profile", "--no-pmc", "--model", args.model, "--batch", str(args.batch), "--prompt",
+               "--no-profile", "--no-pmc", "--no-pipeline-n1", "--model", args.model, "--batch", str(args.batch), "--prompt",
                str(args.prompt), "--dtype", args.dtype, "--seed", str(args.seed),
                "--weights", args.weights]
         try:
@@ -149,7 +154,7 @@ def cpu_baseline(model, steps, seed, ranges=None):
     from distributed_inference_demo_amd.placement import stage_ranges
     from oracle.oracle import num_threads
     ranges = ranges or [(0, model.n_layer)]
-    n_ref, n_ctx = max(2, steps // 6), 16 + 3 + steps + 4
+    n_ref, n_ctx = max(8, steps // 3), 16 + 3 + 1 + max(steps, max(8, steps // 3)) + 4
     t0 = time.perf_counter()
     st = _cpu_stages(model, ranges, n_ctx, seed)
     t_init = time.perf_counter() - t0
@@ -160,14 +165,18 @@ def cpu_baseline(model, steps, seed, ranges=None):
     r560 = stage_ranges(2, m560.n_layer)
     st = _cpu_stages(m560, r560, n_ctx, seed)
     kv560 = _run_cpu_stages(m560, st, 16, steps, "cpu-kv")
-    ref560 = _run_cpu_stages(m560, st, 16, max(2, steps // 4), "cpu-ref")
+    ref560 = _run_cpu_stages(m560, st, 16, n_ref, "cpu-ref")
     del st
     host = _host_info()
-    return {"value": kv, "unit": "tokens/s", "cores": num_threads(), "kind": "port",
+    thr = num_threads()
+    return {"value": kv, "unit": "tokens/s", "cores": thr, "kind": "port",
             "sample": f"{model.name} fp32 C restatement (oracle/bloom_oracle.c), stages {ranges} joined by the "
-                      f"utils.cpp wire format, batch 1, cpu-kv: {steps} decode tokens after a 16-token prompt "
-                      f"(3 warm-up tokens excluded), {num_threads()} OpenMP threads; weight generation {t_init:.1f}s "
-                      "excluded",
+                      f"utils.cpp wire format, batch 1, cpu-kv: {steps} decode tokens after a 16-token prompt, "
+                      f"cpu-ref: {n_ref} tokens each recomputing the whole sequence (3 warm-up tokens excluded), "
+                      f"{thr} OpenMP threads; weight generation {t_init:.1f}s excluded",
+            "threads_note": (f"{thr} OpenMP threads = OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}: "
+                             "the GPU box's CPU share per GPU (the harness sets it and asks that worker pools be "
+                             "sized to it); nproc / affinity_cpus count the whole host"),
             "modes": {"cpu-kv": kv, "cpu-ref": ref},
             "configs0_bloom560m_2stage_loopback": {"stages": r560, "cpu-kv": kv560, "cpu-ref": ref560,
                                                    "unit": "tokens/s", "prompt": 16},
@@ -196,6 +205,16 @@ def hbm_measured(dev):
     torch.cuda.empty_cache()
     return {"read_GBps": rd, "copy_GBps": cp, "torch_copy_GBps": 2 * 2 * n / (best * 1e-3) / 1e9,
             "method": "bs_hbm_probe: 2 GiB, 16-B non-temporal loads (8 in flight per thread), 2048 x 256 threads, best of 10, HIP events"}
+
+
+def mfma_measured(dev):
+    """Measured dense bf16 MFMA rate (re-measure the vendor peaks on the box): bs_mfma_probe,
+    register-operand MFMA chains on every CU, best of 5."""
+    from distributed_inference_demo_amd.stage import mfma_probe
+    a, b = mfma_probe(dev.index or 0)
+    return {"bf16_TFLOPs": max(a, b), "v_mfma_f32_32x32x16_bf16": a, "v_mfma_f32_16x16x32_bf16": b,
+            "method": "bs_mfma_probe: 8 independent accumulator chains per wave, 8 waves per CU, no memory "
+                      "traffic, best of 5, HIP events"}
 
 
 def _cpu_model():
@@ -314,8 +333,10 @@ def bench_single(args):
         res["roofline"]["peak_measured_read"] = hbm["read_GBps"]
         res["roofline"]["frac_of_measured_read"] = res["roofline"]["achieved"] / hbm["read_GBps"]
     res["stage_hbm"]["frac_of_measured_read"] = res["stage_hbm"]["achieved_GBps"] / hbm["read_GBps"]
-    if args.cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(m, args.cpu_steps, args.seed)
+    mf = mfma_measured(dev)
+    res["mfma_measured"] = dict(mf, vendor_peak_TFLOPs=BF16_PEAK_TFLOPS)
+    if "gemm_TFLOPs" in res["prefill"]:
+        res["prefill"]["gemm_frac_of_measured_peak"] = res["prefill"]["gemm_TFLOPs"] / mf["bf16_TFLOPs"]
     return res
 
 
@@ -324,16 +345,46 @@ def _prompt(B, P, V):
     return prompt_ids(1234, B, P, V)
 
 
+def _pipeline_n1(args):
+    """The pipeline code (pipeline.bench_pipeline) at N = 1 on an nccl world-1 group: the point the driver's
+    N > 1 lines (the same code under torchrun) scale from."""
+    import socket
+    from distributed_inference_demo_amd.pipeline import bench_pipeline
+    if "MASTER_PORT" not in os.environ:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+        s.close()
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    os.environ.setdefault("LOCAL_RANK", "0")
+    return bench_pipeline(args)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 or args.gpus > 1:
-        from distributed_inference_demo_amd.pipeline import bench_pipeline
-        res, ranges, model = bench_pipeline(args)
-        if res is not None and args.cpu_baseline:  # rank 0, after the process group is gone
-            res["cpu_baseline"] = cpu_baseline(model, args.cpu_steps, args.seed, ranges=ranges)
+    ranges = model = None
+    if world > 1 or args.gpus > 1 or args.pipeline:
+        if world == 1:
+            res, ranges, model = _pipeline_n1(args)
+        else:
+            from distributed_inference_demo_amd.pipeline import bench_pipeline
+            res, ranges, model = bench_pipeline(args)
     else:
         res = bench_single(args)
+        if not args.no_pipeline_n1:
+            p1, _, _ = _pipeline_n1(args)
+            res["pipeline_n1"] = {k: p1[k] for k in ("value", "ms_per_step", "config", "weak_definition", "stage_hbm",
+                                                     "prefill") if k in p1}
+            if "strong" in p1:
+                res["pipeline_n1"]["strong"] = p1["strong"]
+            res["pipeline_n1"]["note"] = ("pipeline.bench_pipeline at N = 1 (nccl world-1 group, StageExecutor, "
+                                          "graph-replayed decode): the same code and definitions as the N > 1 lines")
+        from distributed_inference_demo_amd import config
+        model = config.get(args.model)
+    if res is not None and args.cpu_baseline:  # rank 0, after the process group is gone
+        res["cpu_baseline"] = cpu_baseline(model, args.cpu_steps, args.seed, ranges=ranges)
     if res is not None:
         print(json.dumps(res), flush=True)
 

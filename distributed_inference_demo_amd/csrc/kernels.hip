@@ -1176,11 +1176,9 @@ static void gemv_tiles_launch(const bf16* X, const WT* W, int M, int N, int K, i
   const size_t shm = sizeof(float) * WAVES * (T * 16) * (MT * 16 + 1);
   const int blocks = (N + T * 16 - 1) / (T * 16);
   const dim3 g(blocks, KS);
-  // interleaved units: +12 % on bloom-7b1 B = 32 decode (profiles/r02_tiles_sweep.txt); BS_TILES_IL=0: contiguous
-  // unit ranges per wave; deeper register rings (PD 3, 4) and 4-k-step units measured slower
-  static const bool il = [] { const char* e = getenv("BS_TILES_IL"); return !(e && *e == '0'); }();
-  if (il) gemv_tiles_kernel<T, MT, WAVES, WT, 2, true><<<g, WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
-  else gemv_tiles_kernel<T, MT, WAVES, WT, 2, false><<<g, WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+  // interleaved units: +12 % on bloom-7b1 B = 32 decode over contiguous unit ranges per wave
+  // (profiles/r02_tiles_sweep.txt); deeper register rings (PD 3, 4) and 4-k-step units measured slower
+  gemv_tiles_kernel<T, MT, WAVES, WT, 2, true><<<g, WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
 }
 
 // Shape choice: the BLOOM shapes take the fastest (tiles, K splits, waves) of the
@@ -1210,21 +1208,6 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
     if (c.N == N && c.K == K) {
       T = M > 16 ? c.T2 : c.T1; KS = M > 16 ? c.KS2 : c.KS1; WV = M > 16 ? c.W2 : c.W1;
     }
-  // BS_TILES_CFG="N,K,T,KS,W/...": per-shape override for M > 16, BS_TILES_CFG1 for M <= 16 (sweeps)
-  auto parse = [](const char* e) {
-    std::vector<std::array<int, 5>> v;
-    while (e && *e) {
-      std::array<int, 5> c{};
-      if (sscanf(e, "%d,%d,%d,%d,%d", &c[0], &c[1], &c[2], &c[3], &c[4]) == 5) v.push_back(c);
-      e = strchr(e, '/');
-      if (e) e++;
-    }
-    return v;
-  };
-  static const std::vector<std::array<int, 5>> ovr2 = parse(getenv("BS_TILES_CFG"));
-  static const std::vector<std::array<int, 5>> ovr1 = parse(getenv("BS_TILES_CFG1"));
-  for (const auto& c : (M > 16 ? ovr2 : ovr1))
-    if (c[0] == N && c[1] == K) { T = c[2]; KS = c[3]; WV = c[4]; }
   const int blocks = (N + T * 16 - 1) / (T * 16);
   const bool sk_ok = ep.sk_ws && ep.sk_tickets && blocks <= ep.sk_ntickets;
   if (WV == 0) {  // not in the table
@@ -1237,11 +1220,9 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
   {
     // gemv_ldsw4 at the table's (T, KS) (bloom-7b1 B=32: qkv 29.7 -> 21.3 us, dense 15.8 -> 12.5, fc1
     // 36.4 -> 25.6, fc2 43.1 -> 32.0; decode steps: 7b1 B=16 +11 %, 3b B=8 +35 %, 1b1 B=8 +32 % over
-    // gemv_tiles; profiles/r02_tiles_sweep.txt).  BS_TILES_LDSW4=0: gemv_tiles only (A/B switch).
-    static const bool l4 = [] { const char* e = getenv("BS_TILES_LDSW4"); return !(e && *e == '0'); }();
-    static const bool l4q = [] { const char* e = getenv("BS_TILES_LDSW4_Q8"); return !(e && *e == '0'); }();
+    // gemv_tiles; profiles/r02_tiles_sweep.txt).  gemv_tiles takes the shapes whose K parts do not divide K.
     constexpr int KC = 128 / (int)sizeof(WT);
-    if (l4 && (sizeof(WT) == 2 || l4q) && T <= 4 && K % (KS * 8 * KC) == 0) {
+    if (T <= 4 && K % (KS * 8 * KC) == 0) {
       auto go4 = [&](auto tc) {
         constexpr int TT = decltype(tc)::value;
         if (two) gemv_ldsw4_launch<TT, 8, 2, WT>(x, w, M, N, K, KS, ep, s);
@@ -1268,12 +1249,6 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
   else if (T == 2) gw(EpiKindC<2>{});
   else gw(EpiKindC<1>{});
   return true;
-}
-
-static bool gemv_tiles_disabled() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("BS_GEMV_TILES_OFF"); v = (e && *e && *e != '0') ? 1 : 0; }
-  return v == 1;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1378,22 +1353,8 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(const bf16* __restrict__
 // with the 16-B chunk index XOR-swizzled by (row & 7), so the 16 rows a ds_read_b128 lane group
 // touches land on different chunk slots.  MFMA v_mfma_f32_16x16x32_bf16.
 // ------------------------------------------------------------------------------------
-// Output tile of this workgroup, XCD-aware.  Dispatch puts workgroup id b on XCD b % 8 and an XCD's
-// 4 MB L2 serves only its own CUs: with the plain row-major tile order every XCD touches every weight
-// row, nothing is re-read from L2 and the whole GEMM streams from the Infinity Cache (bloom-1b1 QKV at
-// 512 tokens: 226 MB of tile loads in 26.7 us = 8.5 TB/s, that cache's rate).  Remapped, XCD x takes a
-// contiguous 1/8 of the column tiles (its weight rows: 1.8 MB for that QKV) against every row tile,
-// so its loads hit its own L2.  BS_GEMM_XCD=1 turns it on (A/B): the L2 hit rate is 88 % either way at
-// bloom-1b1 prefill sizes (profiles/r02_gemm_pmc.txt), so it is off.
-__device__ __forceinline__ void gemm_tile_xcd(int BM, int BN, int xcd, int& m0, int& n0) {
-  const int gx = gridDim.x, gy = gridDim.y, nb = gx * gy;
-  const int lid = blockIdx.x + blockIdx.y * gx;
-  const int per = nb >> 3;
-  int t = lid;
-  if (xcd && lid < per * 8) t = (lid & 7) * per + (lid >> 3);
-  if (xcd) { m0 = (t % gy) * BM; n0 = (t / gy) * BN; }
-  else { m0 = blockIdx.y * BM; n0 = blockIdx.x * BN; }
-}
+// Tile order: row-major (an XCD-major remap that keeps each XCD's weight rows in its own L2 measured no
+// gain: the L2 hit rate is 88 % either way at bloom-1b1 prefill sizes, profiles/r02_gemm_pmc.txt).
 
 // Epilogue operands of one GEMM thread, loaded before the K loop (they do not depend on the sums):
 // bias and int8 column scale per output column j, the residual per element, the cached positions per
@@ -1484,7 +1445,7 @@ __device__ __forceinline__ void gemm_epi_store(const f32x4 (&acc)[TM][TN], const
 
 template <int BM, int BN, int PS, int EK>
 __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
-                                                         int M, int N, int K, Epi ep, int xcd) {
+                                                         int M, int N, int K, Epi ep) {
   constexpr int BK = 64;
   constexpr int TM = BM / 32, TN = BN / 32;           // 16x16 tiles per wave (wave = BM/2 x BN/2)
   constexpr int CA = BM * BK / 8 / 256, CB = BN * BK / 8 / 256;  // 16-B chunks per thread: 4, 4|2|1
@@ -1492,8 +1453,7 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
   __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * BK];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1, r = lane & 15, g = lane >> 4;
-  int m0, n0;
-  gemm_tile_xcd(BM, BN, xcd, m0, n0);
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   auto sw = [](int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); };  // element offset
   auto row_m = [&](int i, int e) { return m0 + wm * (BM / 2) + i * 16 + 4 * g + e; };
   auto col_n = [&](int j) { return n0 + wn * (BN / 2) + j * 16 + r; };
@@ -1589,13 +1549,13 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
 
 // gemm_mfma2_kernel with the epilogue kind as a template argument.
 template <int BM, int BN, int PS>
-static void gemm2_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int xcd) {
+static void gemm2_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s) {
   const dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
   switch (ep.kind) {
-    case EPI_QKV: gemm_mfma2_kernel<BM, BN, PS, EPI_QKV><<<grid, 256, 0, s>>>(x, w, M, N, K, ep, xcd); break;
-    case EPI_RESID: gemm_mfma2_kernel<BM, BN, PS, EPI_RESID><<<grid, 256, 0, s>>>(x, w, M, N, K, ep, xcd); break;
-    case EPI_GELU: gemm_mfma2_kernel<BM, BN, PS, EPI_GELU><<<grid, 256, 0, s>>>(x, w, M, N, K, ep, xcd); break;
-    default: gemm_mfma2_kernel<BM, BN, PS, EPI_ARGMAX><<<grid, 256, 0, s>>>(x, w, M, N, K, ep, xcd); break;
+    case EPI_QKV: gemm_mfma2_kernel<BM, BN, PS, EPI_QKV><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_RESID: gemm_mfma2_kernel<BM, BN, PS, EPI_RESID><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_GELU: gemm_mfma2_kernel<BM, BN, PS, EPI_GELU><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
+    default: gemm_mfma2_kernel<BM, BN, PS, EPI_ARGMAX><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
   }
 }
 
@@ -1622,30 +1582,6 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   epi_dispatch(ep.kind, [&](auto kc) {
     epi_apply<float, decltype(kc)::value>(ep, m, n, acc, m < M && n < N, (N + 15) >> 4);
   });
-}
-
-static int gemm_xcd() {  // BS_GEMM_XCD=1: XCD-major tile order (A/B switch; off: measured no gain)
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("BS_GEMM_XCD"); v = (e && *e == '1') ? 1 : 0; }
-  return v;
-}
-
-static bool gemm_v1_forced() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("BS_GEMM_V1"); v = (e && *e && *e != '0') ? 1 : 0; }
-  return v == 1;
-}
-
-static bool gemm_no_narrow() {  // BS_GEMM_NO_NARROW=1: keep 64x64 prefill tiles (A/B switch)
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("BS_GEMM_NO_NARROW"); v = (e && *e && *e != '0') ? 1 : 0; }
-  return v == 1;
-}
-
-static bool gemv_rows_disabled() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("BS_GEMV_MFMA"); v = (e && *e && *e != '0') ? 1 : 0; }
-  return v == 1;
 }
 
 template <int WAVES, int MT, bool LN>
@@ -1682,13 +1618,8 @@ static void gemv_rows_launch(const bf16* X, const LnArgs& ln, const AttnParts& p
 // on some CUs and 2 on others (bloom-1b1 QKV: 576 blocks) ends when the 3-block CUs do: the in-kernel
 // timeline (tools/gemv_timeline.hip) showed 2 us between the first and last block's end.  Here a block
 // holds ceil(N / 256) rows (R per wave, <= 16 waves), so the grid is ~256 equal blocks.
-static bool rows_per_cu_enabled() {  // BS_ROWS_CU=0: the old fixed 4-wave blocks (A/B switch)
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("BS_ROWS_CU"); v = (e && *e == '0') ? 0 : 1; }
-  return v == 1;
-}
 static void rows_geometry(int N, int K, int M, int r_default, int* R, int* waves) {
-  if (!rows_per_cu_enabled() || M > 2) { *R = r_default; *waves = 4; return; }
+  if (M > 2) { *R = r_default; *waves = 4; return; }
   const int rows_cu = (N + 255) / 256;
   int r = K <= 2048 ? 2 : 1;
   while ((rows_cu + r - 1) / r > 16 && r < 4) r *= 2;
@@ -1704,8 +1635,7 @@ static void rows_plan(int XM, int M, int N, int K, int* R, int* waves, int* U) {
   // variants 2-4 on wide N to amortise the per-block LayerNorm prologue
   // LN-fused: >= 2 rows per wave halves the blocks that each redo the row's LayerNorm
   // (profiles/r01_ln_rows_sweep.txt: 560m 1566 -> 1621 tok/s, 1b1 1229 -> 1242)
-  static const int plain_r = [] { const char* e = getenv("BS_PLAIN_R"); return e && *e ? atoi(e) : 0; }();  // sweeps
-  const int R0 = !LN ? (plain_r ? plain_r : (K <= 2048 ? 2 : 1)) : (N >= 12288 ? 4 : (N >= 2048 ? 2 : 1));
+  const int R0 = !LN ? (K <= 2048 ? 2 : 1) : (N >= 12288 ? 4 : (N >= 2048 ? 2 : 1));
   rows_geometry(N, K, M, R0, R, waves);
   // U = 512-element chunks of a row in flight per iteration: an exact divisor of the row's chunk
   // count, so every row streams in whole rounds with no re-loaded tail (K = 1536 -> 3, 6144 -> 12,
@@ -1777,8 +1707,8 @@ static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const AttnParts&
 template <bool LN>
 static void gemv_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, int M, int N, int K, const Epi& ep,
                           hipStream_t s) {
-  if (!gemv_rows_disabled() && gemv_rows_dispatch<LN ? X_LN : X_PLAIN>(x, ln, AttnParts{}, w, M, N, K, ep, s)) return;
-  if (!LN && !gemv_tiles_disabled() && gemv_tiles_dispatch(x, w, M, N, K, ep, s)) return;
+  if (gemv_rows_dispatch<LN ? X_LN : X_PLAIN>(x, ln, AttnParts{}, w, M, N, K, ep, s)) return;
+  if (!LN && gemv_tiles_dispatch(x, w, M, N, K, ep, s)) return;
   const int waves = gemv_waves(N, K);
   const bool two = M > 16;
   if (waves == 4) { if (two) gemv_launch<4, 2, LN>(x, ln, w, M, N, K, ep, s); else gemv_launch<4, 1, LN>(x, ln, w, M, N, K, ep, s); }
@@ -1794,7 +1724,7 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
   if (M <= 0) return;
   // 4 < M <= 32: a LayerNorm kernel + the tile GEMV beats the per-tile LN-fused GEMV
   // (tools/gemv_probe.hip batched section)
-  const bool tiles = is_bf16 && M > 4 && M <= 32 && (K % 64) == 0 && !gemv_tiles_disabled();
+  const bool tiles = is_bf16 && M > 4 && M <= 32 && (K % 64) == 0;
   if (is_bf16 && M <= 8 && (K % 8) == 0 && !tiles) {
     LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
     gemv_dispatch<true>(nullptr, ln, (const bf16*)W, M, N, K, ep, s);
@@ -1817,7 +1747,7 @@ bool linear_parts_supported(int M, int K, int head_dim, int nsplit) {
 bool launch_linear_emb(const int* ids, const void* wemb, const void* emb_g, const void* emb_b, float* x_out,
                        const void* gamma, const void* beta, float eps, const void* W, int M, int N, int K,
                        const Epi& ep, hipStream_t s) {
-  if (M < 1 || M > 2 || gemv_rows_disabled()) return false;
+  if (M < 1 || M > 2) return false;
   LnArgs ln{nullptr, 1, 0, (const bf16*)gamma, (const bf16*)beta, eps,
             ids, (const bf16*)wemb, (const bf16*)emb_g, (const bf16*)emb_b, x_out};
   return gemv_rows_dispatch<X_EMB>(nullptr, ln, AttnParts{}, (const bf16*)W, M, N, K, ep, s);
@@ -1841,31 +1771,19 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
     gemv_dispatch<false>(x, LnArgs{}, w, M, N, K, ep, s);
     return;
   }
-  if ((K % 64) == 0 && !gemm_v1_forced()) {
+  if ((K % 64) == 0) {
     // 128x128 when it still gives every CU a block (>= 240 blocks), else 64x64, else 64x32
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-    static const int forced = [] {  // BS_GEMM_TILE=1..4: force 128x128 / 128x64 / 64x64 / 64x32 (sweeps)
-      const char* e = getenv("BS_GEMM_TILE");
-      return e && *e ? atoi(e) : 0;
-    }();
-    if (forced == 1) {
-      gemm2_launch<128, 128, 1>(x, w, M, N, K, ep, s, gemm_xcd());
-    } else if (forced == 2) {
-      gemm2_launch<128, 64, 3>(x, w, M, N, K, ep, s, gemm_xcd());
-    } else if (forced == 3) {
-      gemm2_launch<64, 64, 4>(x, w, M, N, K, ep, s, gemm_xcd());
-    } else if (forced == 4) {
-      gemm2_launch<64, 32, 4>(x, w, M, N, K, ep, s, gemm_xcd());
-    } else if (blocks(128, 128) >= 240) {
-      gemm2_launch<128, 128, 1>(x, w, M, N, K, ep, s, gemm_xcd());
-    } else if (blocks(64, 64) >= 240 || gemm_no_narrow()) {
+    if (blocks(128, 128) >= 240) {
+      gemm2_launch<128, 128, 1>(x, w, M, N, K, ep, s);
+    } else if (blocks(64, 64) >= 240) {
       // below 240 128x128 tiles the K loop is latency-bound: 64x64 tiles with a 4-deep ring beat
       // 128x64 (profiles/r01_gemm_tile_sweep.txt: bloom-1b1 S=512 prefill 4.56 -> 4.42 ms)
-      gemm2_launch<64, 64, 4>(x, w, M, N, K, ep, s, gemm_xcd());
+      gemm2_launch<64, 64, 4>(x, w, M, N, K, ep, s);
     } else {
       // narrow N at prefill sizes (bloom-1b1 dense / fc2 at 512 tokens: 192 64x64 tiles): 64x32
       // tiles put >= 1 block on every CU, and a second block on many, to hide the K loop's loads
-      gemm2_launch<64, 32, 4>(x, w, M, N, K, ep, s, gemm_xcd());
+      gemm2_launch<64, 32, 4>(x, w, M, N, K, ep, s);
     }
     return;
   }
@@ -2342,33 +2260,13 @@ size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, 
 // otherwise 4-wave blocks split the context so ~256 blocks stream the KV cache (>= one 64-position
 // chunk per wave at full cache).  Static per (B, n_head, cache size), so the consumer of a deferred
 // merge knows it without a device round trip.
-// Wide decode attention (few (row, head) pairs): 2-wave blocks of 32-position chunks, one block per 64
-// cached positions, so the KV stream spreads over ~all CUs (a CU pulls ~24 GB/s of a chip-wide stream:
-// 48 blocks for bloom-1b1 B = 1 left 70 KB of K/V per CU, ~3 us); the last split block of each
-// (row, head) merges by ticket and writes ctx, so the dense GEMV after it needs no merge prologue.
-// Measured (profiles/r02_attn_wide_ab.txt): bloom-7b1 B = 1 ctx ~200 +1.7 %, bloom-1b1 B = 1 ctx ~600 -4 %
-// (the ticket merge's atomic + reload round trips on the last block cost more than the narrow kernel's
-// per-CU stream); off by default, BS_ATTN_WIDE=1 turns it on.
-static bool attn_wide() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("BS_ATTN_WIDE"); v = (e && *e == '1') ? 1 : 0; }
-  return v == 1;
-}
-
+// A wide variant (2-wave blocks of 32 positions, one block per 64 cached positions, ticket merge in the
+// launch) measured bloom-7b1 B = 1 +1.7 %, bloom-1b1 B = 1 -4 % (profiles/r02_attn_wide_ab.txt): removed.
 int attention_decode_splits(int B, int n_head, int max_chunks) {
-  static const int forced = [] { const char* e = getenv("BS_ATTN_SPLITS"); return e && *e ? atoi(e) : 0; }();  // sweeps
-  if (forced > 0) return min(forced, max(1, max_chunks));
   const int pairs = B * n_head;
   if (pairs >= 192 || max_chunks <= 4) return 1;
-  if (attn_wide()) return max(1, min(max_chunks, 512 / pairs));
   const int nsplit = min((256 + pairs - 1) / pairs, (max_chunks + 3) / 4);
   return max(1, min(nsplit, 64));
-}
-
-static bool attn_small_chunks() {  // BS_ATTN_CH64=1: keep 4 waves x 64 positions (A/B switch)
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("BS_ATTN_CH64"); v = (e && *e && *e != '0') ? 0 : 1; }
-  return v == 1;
 }
 
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
@@ -2380,10 +2278,7 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
       dim3 g(a.n_head, a.B, 1);
       if (is_bf16) attn_decode_kernel<bf16, 8><<<g, 512, 0, s>>>(a);
       else attn_decode_kernel<float, 8><<<g, 512, 0, s>>>(a);
-    } else if (is_bf16 && !a.defer_merge && attn_wide()) {
-      dim3 g(a.n_head, a.B, nsplit);
-      attn_decode_kernel<bf16, 2, 32><<<g, 128, 0, s>>>(a);
-    } else if (is_bf16 && a.defer_merge && attn_small_chunks()) {
+    } else if (is_bf16 && a.defer_merge) {
       // few (row, head) pairs: 8 waves x 32 positions per block, half the serial work per wave
       dim3 g(a.n_head, a.B, nsplit);
       attn_decode_kernel<bf16, 8, 32><<<g, 512, 0, s>>>(a);
@@ -2396,12 +2291,7 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
     if (is_bf16 && a.head_dim <= 128) {
       dim3 g((a.S + 63) / 64, a.n_head, a.B);
       const int hdp = (a.head_dim + 31) / 32 * 32;
-      static const bool plo = [] { const char* e = getenv("BS_ATTN_PLO"); return !(e && *e == '0'); }();  // A/B
-      if (!plo) {
-        if (hdp <= 64) attn_prefill_mfma_kernel<64, false><<<g, 256, 0, s>>>(a);
-        else if (hdp <= 96) attn_prefill_mfma_kernel<96, false><<<g, 256, 0, s>>>(a);
-        else attn_prefill_mfma_kernel<128, false><<<g, 256, 0, s>>>(a);
-      } else if (hdp <= 64) attn_prefill_mfma_kernel<64><<<g, 256, 0, s>>>(a);
+      if (hdp <= 64) attn_prefill_mfma_kernel<64><<<g, 256, 0, s>>>(a);
       else if (hdp <= 96) attn_prefill_mfma_kernel<96><<<g, 256, 0, s>>>(a);
       else attn_prefill_mfma_kernel<128><<<g, 256, 0, s>>>(a);
     } else {
@@ -2818,47 +2708,25 @@ __global__ __launch_bounds__(WIDE ? 1024 : 256) void gemv_q8_kernel(const int8_t
   });
 }
 
-// Bytes per lane per weight row and step: BS_Q8_CW=16|32 (A/B knob), default 16.
-static int q8_cw() {
-  static const int v = [] {
-    const char* e = getenv("BS_Q8_CW");
-    return e && atoi(e) == 32 ? 32 : 16;
-  }();
-  return v;
-}
-
 template <int R, int MM, bool LN = false, bool PARTS = false>
 static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, const LnArgs& ln, int M, int N, int K,
                            const Epi& ep, hipStream_t s, const AttnParts& pa = AttnParts{}) {
-  static const bool xl = [] {  // BS_Q8_XL=1: plain X staged in LDS when it fits 64 KB (A/B knob)
-    const char* e = getenv("BS_Q8_XL");
-    return e && *e == '1';
-  }();
-  const bool stage_x = !LN && !PARTS && xl && (size_t)M * K * sizeof(bf16) <= 65536;
-  const size_t shm = (LN || PARTS || stage_x) ? (size_t)M * K * sizeof(bf16) : 0;
+  const size_t shm = (LN || PARTS) ? (size_t)M * K * sizeof(bf16) : 0;
   const int blocks = (N + 4 * R - 1) / (4 * R);
   // steps of every row in flight: the whole row (<= 8 steps of 64 x 16 B) for matrices up to 12 M weights,
   // where the grid is a few waves per SIMD and latency decides (bloom-1b1 int8 B=1: 1207 -> 1221 tok/s);
   // one step beyond, where the stream is bandwidth-bound and deeper queues only cost occupancy
   // (bloom-7b1 int8: UQ=1 486.6, UQ=2 471.7, the whole row 454 tok/s; profiles/r02_q8_uq_ab.txt)
-  static const int uq_env = [] { const char* e = getenv("BS_Q8_UQ"); return e && *e ? atoi(e) : 0; }();  // A/B
   const int steps = (K + 1023) / 1024;
-  const int uq = uq_env ? uq_env : (size_t)N * K > (12u << 20) ? 1 : min(steps <= 2 ? 2 : steps <= 4 ? 4 : steps <= 6 ? 6 : 8, R >= 4 ? 4 : 8);
-  if constexpr (!LN && !PARTS) {
-    if (stage_x) {
-      gemv_q8_kernel<R, MM, false, 16, true><<<blocks, 256, shm, s>>>(Q, scale, X, ln, pa, M, N, K, ep);
-      return;
-    }
-  }
-  static const bool wide_on = [] { const char* e = getenv("BS_Q8_WIDE"); return !(e && *e == '0'); }();  // A/B
-  static const bool wide_xl_on = [] { const char* e = getenv("BS_Q8_WIDE_XL"); return !(e && *e == '0'); }();  // A/B
-  const bool wide_xl = wide_xl_on && (size_t)M * K * sizeof(bf16) <= 65536;
+  const int uq = (size_t)N * K > (12u << 20) ? 1 : min(steps <= 2 ? 2 : steps <= 4 ? 4 : steps <= 6 ? 6 : 8, R >= 4 ? 4 : 8);
+  // plain X staged in LDS (loaded ahead of the weights) by the wide blocks when it fits 64 KB
+  const bool wide_xl = (size_t)M * K * sizeof(bf16) <= 65536;
   if constexpr (MM == 1 && R <= 2) {
     int rr = 0, waves = 0;
     rows_geometry(N, K, M, R, &rr, &waves);
     // matrices up to 32 M weights (bloom-1b1 int8 B=1 1206 -> 1281 tok/s, 560m 1685 -> 1768, 3b 735 -> 762;
     // bloom-7b1's 50-67 M-weight QKV / fc1 / fc2 keep 4-wave blocks; profiles/r02_q8_uq_ab.txt)
-    if (wide_on && (size_t)N * K <= (32u << 20) && rr <= 2 && waves >= 4 && uq <= 6) {
+    if ((size_t)N * K <= (32u << 20) && rr <= 2 && waves >= 4 && uq <= 6) {
       auto go = [&](auto rc) {
         constexpr int RW = decltype(rc)::value;
         const int wb = (N + waves * RW - 1) / (waves * RW);
@@ -2899,14 +2767,7 @@ static void gemv_q8_launch(const int8_t* Q, const float* scale, const bf16* X, c
 bool linear_q8_gemv(int M, int K) { return M >= 1 && M <= 8 && K % 32 == 0; }
 
 // Rows per wave of the int8 GEMV: 2 (profiles/r01_q8_rows_sweep.txt: 1b1 B=1 1128 -> 1177 tok/s against 1 row
-// below N = 8192, 7b1 equal); BS_Q8_R=1|2|4 forces it (4 only at M = 1).
-static int q8_rows(int N) {
-  static const int forced = [] {
-    const char* e = getenv("BS_Q8_R");
-    return e && *e ? atoi(e) : 0;
-  }();
-  return forced ? forced : 2;
-}
+// below N = 8192, 7b1 equal).
 bool linear_q8_ln_fused(int M, int K) { return M >= 1 && M <= 4 && K % 32 == 0 && K <= 4096; }
 
 void launch_linear_q8_ln(const float* x, int row_stride, int row_offset, const void* gamma, const void* beta,
@@ -2915,15 +2776,9 @@ void launch_linear_q8_ln(const float* x, int row_stride, int row_offset, const v
   Epi e = ep;
   e.col_scale = scale;
   const LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
-  const int rr = q8_rows(N);
-  const bool r2 = rr >= 2;
-  if (M <= 1 && rr == 4) gemv_q8_launch<4, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s);
-  else if (M <= 1) r2 ? gemv_q8_launch<2, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s)
-                   : gemv_q8_launch<1, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s);
-  else if (M <= 2) r2 ? gemv_q8_launch<2, 2, true>(Q, scale, nullptr, ln, M, N, K, e, s)
-                   : gemv_q8_launch<1, 2, true>(Q, scale, nullptr, ln, M, N, K, e, s);
-  else r2 ? gemv_q8_launch<2, 4, true>(Q, scale, nullptr, ln, M, N, K, e, s)
-          : gemv_q8_launch<1, 4, true>(Q, scale, nullptr, ln, M, N, K, e, s);
+  if (M <= 1) gemv_q8_launch<2, 1, true>(Q, scale, nullptr, ln, M, N, K, e, s);
+  else if (M <= 2) gemv_q8_launch<2, 2, true>(Q, scale, nullptr, ln, M, N, K, e, s);
+  else gemv_q8_launch<2, 4, true>(Q, scale, nullptr, ln, M, N, K, e, s);
 }
 
 bool linear_q8_parts_supported(int M, int K, int head_dim, int nsplit) {
@@ -2934,8 +2789,7 @@ void launch_linear_q8_parts(const AttnParts& p, const int8_t* Q, const float* sc
                             const Epi& ep, hipStream_t s) {
   Epi e = ep;
   e.col_scale = scale;
-  if (M <= 1 && q8_rows(N) == 4) gemv_q8_launch<4, 1, false, true>(Q, scale, nullptr, LnArgs{}, M, N, K, e, s, p);
-  else if (M <= 1) gemv_q8_launch<2, 1, false, true>(Q, scale, nullptr, LnArgs{}, M, N, K, e, s, p);
+  if (M <= 1) gemv_q8_launch<2, 1, false, true>(Q, scale, nullptr, LnArgs{}, M, N, K, e, s, p);
   else gemv_q8_launch<2, 2, false, true>(Q, scale, nullptr, LnArgs{}, M, N, K, e, s, p);
 }
 
@@ -2968,15 +2822,12 @@ void launch_linear_q8(const void* X, const int8_t* Q, const float* scale, void* 
   e.col_scale = scale;
   // batched decode (4 < M <= 32): the int8 gemv_ldsw4 / tile GEMV converts in registers (no dequant pass);
   // at M = 8 it reads the weights once where gemv_q8 re-reads activations per row (bloom-7b1 int8 B=8)
-  if (M > 4 && M <= 32 && !gemv_tiles_disabled() && gemv_tiles_dispatch<int8_t>(x, Q, M, N, K, e, s)) return;
+  if (M > 4 && M <= 32 && gemv_tiles_dispatch<int8_t>(x, Q, M, N, K, e, s)) return;
   if (linear_q8_gemv(M, K)) {
-    const int rr = q8_rows(N);
-    const bool r2 = rr >= 2;
     const LnArgs ln{};
-    if (M <= 1 && rr == 4) gemv_q8_launch<4, 1>(Q, scale, x, ln, M, N, K, e, s);
-    else if (M <= 1) r2 ? gemv_q8_launch<2, 1>(Q, scale, x, ln, M, N, K, e, s) : gemv_q8_launch<1, 1>(Q, scale, x, ln, M, N, K, e, s);
-    else if (M <= 2) r2 ? gemv_q8_launch<2, 2>(Q, scale, x, ln, M, N, K, e, s) : gemv_q8_launch<1, 2>(Q, scale, x, ln, M, N, K, e, s);
-    else if (M <= 4) r2 ? gemv_q8_launch<2, 4>(Q, scale, x, ln, M, N, K, e, s) : gemv_q8_launch<1, 4>(Q, scale, x, ln, M, N, K, e, s);
+    if (M <= 1) gemv_q8_launch<2, 1>(Q, scale, x, ln, M, N, K, e, s);
+    else if (M <= 2) gemv_q8_launch<2, 2>(Q, scale, x, ln, M, N, K, e, s);
+    else if (M <= 4) gemv_q8_launch<2, 4>(Q, scale, x, ln, M, N, K, e, s);
     else gemv_q8_launch<1, 8>(Q, scale, x, ln, M, N, K, e, s);
     return;
   }

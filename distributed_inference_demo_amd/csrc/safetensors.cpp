@@ -236,6 +236,9 @@ bool Checkpoint::map_file(const std::string& path, std::string* err) {
   uint64_t hlen = 0;
   for (int i = 0; i < 8; i++) hlen |= (uint64_t)b[i] << (8 * i);
   if (hlen > len - 8) { *err = "header length past the end of " + path; return false; }
+  // the upstream safetensors format caps the JSON header at 100 MB; a larger one is not a checkpoint
+  // (and would only make the recursive parser build a huge tree from untrusted input)
+  if (hlen > (100ull << 20)) { *err = "safetensors header of " + std::to_string(hlen) + " B exceeds the 100 MB cap in " + path; return false; }
   Value root;
   if (!Parser((const char*)b + 8, (size_t)hlen).parse(&root) || root.kind != Value::OBJ) {
     *err = "malformed safetensors header: " + path;

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/bloomstage.h"
+#include "common.h"
 #include "kernels.h"
 #include "safetensors.h"
 
@@ -117,6 +118,7 @@ struct bs_stage {
   unsigned* att_tickets = nullptr;     // [max_batch][n_head]
   std::vector<int> past_next;          // what past_dev[0..B) holds after the enqueued forwards (last stage)
   bool past_next_valid = false;
+  hipStream_t past_stream = nullptr;   // the stream those forwards were enqueued on
   float* sk_ws = nullptr;              // batched-GEMV split-K partials (kSkCap floats)
   unsigned* sk_tickets = nullptr;      // [kSkTickets]
   ProfClass prof;
@@ -663,6 +665,34 @@ extern "C" int bs_read_weights(const bs_stage* s, uint64_t offset, uint64_t coun
   return BS_OK;
 }
 
+extern "C" int bs_read_kv(const bs_stage* s, int32_t layer, int32_t slot, int32_t pos0, int32_t npos, float* out) {
+  if (!s || !out) return fail(BS_ERR_INVALID, "stage/out is NULL");
+  if (layer < 0 || layer >= s->L) return fail(BS_ERR_INVALID, "layer outside the stage");
+  if (slot < 0 || slot >= s->d.max_batch) return fail(BS_ERR_INVALID, "slot out of range");
+  if (pos0 < 0 || npos < 0 || pos0 + npos > s->d.max_ctx) return fail(BS_ERR_INVALID, "positions outside max_ctx");
+  HIP_TRY(hipSetDevice(s->d.device));
+  HIP_TRY(hipStreamSynchronize(s->own));
+  const int nh = s->d.n_head, hd = s->hd;
+  const size_t run = (size_t)npos * hd;  // contiguous elements of one (K|V, head)
+  std::vector<uint16_t> tmp(s->bf16 ? run : 0);
+  for (int w = 0; w < 2; w++)
+    for (int hh = 0; hh < nh; hh++) {
+      const size_t e0 = (((size_t)slot * nh + hh) * s->d.max_ctx + pos0) * hd;
+      const char* src = s->kv + layer * s->kv_layer_stride + w * s->kv_half + e0 * s->esz;
+      float* dst = out + ((size_t)w * nh + hh) * run;
+      if (s->bf16) {
+        HIP_TRY(hipMemcpy(tmp.data(), src, run * 2, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < run; i++) {
+          const uint32_t u = (uint32_t)tmp[i] << 16;
+          std::memcpy(&dst[i], &u, 4);
+        }
+      } else {
+        HIP_TRY(hipMemcpy(dst, src, run * 4, hipMemcpyDeviceToHost));
+      }
+    }
+  return BS_OK;
+}
+
 extern "C" int bs_reset_kv(bs_stage* s, int32_t slot) {
   if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
   if (slot >= s->d.max_batch) return fail(BS_ERR_INVALID, "slot out of range");
@@ -757,45 +787,131 @@ __global__ __launch_bounds__(256) void probe_copy_kernel(const probe_u4* __restr
   }
 }
 
+// Probe resources released on every exit path; every HIP call's status is checked.
+namespace {
+struct ProbeRes {
+  void* buf[2] = {nullptr, nullptr};
+  hipStream_t st = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  ~ProbeRes() {
+    if (st) hipStreamSynchronize(st);
+    for (auto e : ev) if (e) hipEventDestroy(e);
+    if (st) hipStreamDestroy(st);
+    for (auto b : buf) if (b) hipFree(b);
+  }
+  int init(size_t bytes, int nbuf) {
+    for (int i = 0; i < nbuf; i++)
+      if (hipMalloc(&buf[i], bytes) != hipSuccess) return fail(BS_ERR_OOM, "probe allocation failed");
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&ev[0]));
+    HIP_TRY(hipEventCreate(&ev[1]));
+    return BS_OK;
+  }
+  // Time one launch (enqueued by `launch`) with the event pair; ms < 0 never escapes (status instead).
+  template <typename F>
+  int timed(F&& launch, float* ms) {
+    HIP_TRY(hipEventRecord(ev[0], st));
+    launch();
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev[1], st));
+    HIP_TRY(hipEventSynchronize(ev[1]));
+    HIP_TRY(hipEventElapsedTime(ms, ev[0], ev[1]));
+    if (!(*ms > 0.f)) return fail(BS_ERR_DEVICE, "probe: non-positive event time");
+    return BS_OK;
+  }
+};
+}  // namespace
+
 extern "C" int bs_hbm_probe(int32_t device, uint64_t bytes, double* read_gbps, double* copy_gbps) {
   if (bytes < (1u << 20) || bytes % (1u << 20)) return fail(BS_ERR_INVALID, "probe bytes must be a positive multiple of 1 MiB");
   HIP_TRY(hipSetDevice(device));
-  void *a = nullptr, *b = nullptr;
-  if (hipMalloc(&a, bytes) != hipSuccess) return fail(BS_ERR_OOM, "probe allocation failed");
-  if (hipMalloc(&b, bytes) != hipSuccess) { hipFree(a); return fail(BS_ERR_OOM, "probe allocation failed"); }
-  hipStream_t st;
-  hipEvent_t e0, e1;
-  hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
-  hipMemsetAsync(a, 1, bytes, st);
+  ProbeRes p;
+  int rc = p.init(bytes, 2);
+  if (rc) return rc;
+  HIP_TRY(hipMemsetAsync(p.buf[0], 1, bytes, p.st));
   const size_t n = bytes / 16;
   const unsigned grid = 256 * 8;  // 8 blocks per CU
+  const probe_u4* a = (const probe_u4*)p.buf[0];
+  probe_u4* b = (probe_u4*)p.buf[1];
   float best_r = 1e30f, best_c = 1e30f;
   for (int it = 0; it < 12; it++) {
-    hipEventRecord(e0, st);
-    probe_read_kernel<<<grid, 256, 0, st>>>((const probe_u4*)a, n, (probe_u4*)b);
-    hipEventRecord(e1, st);
-    hipEventSynchronize(e1);
-    float ms;
-    hipEventElapsedTime(&ms, e0, e1);
+    float ms = 0.f;
+    if ((rc = p.timed([&] { probe_read_kernel<<<grid, 256, 0, p.st>>>(a, n, b); }, &ms))) return rc;
     if (it >= 2) best_r = std::min(best_r, ms);
-    hipEventRecord(e0, st);
-    probe_copy_kernel<<<grid, 256, 0, st>>>((const probe_u4*)a, (probe_u4*)b, n);
-    hipEventRecord(e1, st);
-    hipEventSynchronize(e1);
-    hipEventElapsedTime(&ms, e0, e1);
+    if ((rc = p.timed([&] { probe_copy_kernel<<<grid, 256, 0, p.st>>>(a, b, n); }, &ms))) return rc;
     if (it >= 2) best_c = std::min(best_c, ms);
   }
-  hipError_t err = hipGetLastError();
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipStreamDestroy(st);
-  hipFree(a);
-  hipFree(b);
-  if (err != hipSuccess) return fail(BS_ERR_DEVICE, std::string("probe: ") + hipGetErrorString(err));
   if (read_gbps) *read_gbps = (double)bytes / (best_r * 1e-3) / 1e9;
   if (copy_gbps) *copy_gbps = 2.0 * (double)bytes / (best_c * 1e-3) / 1e9;
+  return BS_OK;
+}
+
+// ---- MFMA probe (bench.py "mfma_measured"): dense bf16 matrix-core rate of this device.
+// Every wave keeps 8 independent accumulator chains of v_mfma_f32_32x32x16_bf16 (16x16x32 for
+// shape = 1) on register operands, 2 waves per SIMD (8 per CU) on a 4-block-per-CU grid: issue-bound
+// on the matrix pipes, no memory traffic.  The result is stored only if it equals a value it never
+// takes, which keeps the chains live.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+template <int SHAPE>
+__global__ __launch_bounds__(128) void probe_mfma_kernel(int iters, float* sink) {
+  const int lane = threadIdx.x & 63;
+  bf16x8 a, b;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    a[j] = (bf16)(1.0f + 0.001f * (float)((lane + j) & 7));
+    b[j] = (bf16)(0.5f - 0.001f * (float)((lane * 3 + j) & 7));
+  }
+  float tot = 0.f;
+  if constexpr (SHAPE == 0) {
+    f32x16 acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) acc[c] = (f32x16){};
+    for (int i = 0; i < iters; i++)
+#pragma unroll
+      for (int c = 0; c < 8; c++) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[c], 0, 0, 0);
+#pragma unroll
+    for (int c = 0; c < 8; c++)
+#pragma unroll
+      for (int j = 0; j < 16; j++) tot += acc[c][j];
+  } else {
+    f32x4 acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) acc[c] = (f32x4){};
+    for (int i = 0; i < iters; i++)
+#pragma unroll
+      for (int c = 0; c < 8; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[c], 0, 0, 0);
+#pragma unroll
+    for (int c = 0; c < 8; c++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) tot += acc[c][j];
+  }
+  if (tot == -1.2345f) sink[blockIdx.x] = tot;
+}
+
+extern "C" int bs_mfma_probe(int32_t device, double* tflops_32x32x16, double* tflops_16x16x32) {
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  ProbeRes p;
+  int rc = p.init(1u << 20, 1);
+  if (rc) return rc;
+  const int iters = 4096, blocks = prop.multiProcessorCount * 4;
+  const double flops_per_iter[2] = {2.0 * 32 * 32 * 16, 2.0 * 16 * 16 * 32};  // per MFMA instruction
+  double best[2] = {0.0, 0.0};
+  for (int shape = 0; shape < 2; shape++) {
+    for (int it = 0; it < 6; it++) {
+      float ms = 0.f;
+      rc = p.timed([&] {
+        if (shape == 0) probe_mfma_kernel<0><<<blocks, 128, 0, p.st>>>(iters, (float*)p.buf[0]);
+        else probe_mfma_kernel<1><<<blocks, 128, 0, p.st>>>(iters, (float*)p.buf[0]);
+      }, &ms);
+      if (rc) return rc;
+      const double fl = (double)blocks * 2 /* waves */ * iters * 8 /* chains */ * flops_per_iter[shape];
+      if (it >= 1) best[shape] = std::max(best[shape], fl / (ms * 1e-3) / 1e12);
+    }
+  }
+  if (tflops_32x32x16) *tflops_32x32x16 = best[0];
+  if (tflops_16x16x32) *tflops_16x16x32 = best[1];
   return BS_OK;
 }
 
@@ -858,16 +974,6 @@ static double gemv_bytes_q8(const bs_stage* s, int M, int N, int K, int out_byte
 }
 
 // Block matrix t of a layer: int8 stages stream the int8 weights (launch_linear_q8).
-// BS_Q8_PARTS=0: the int8 stage's split decode attention merges in its own kernel (ticket) instead of
-// the int8 dense GEMV's prologue (A/B knob)
-static bool q8_parts_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("BS_Q8_PARTS");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-
 static void wlinear(bs_stage* s, hipStream_t st, const void* X, const Layer& w, int t, int M, int N, int K,
                     const Epi& ep, int out_bytes) {
   if (!w.sc[t]) {
@@ -912,16 +1018,6 @@ static int logits_staging(bs_stage* s, size_t bytes, hipStream_t st, float** out
   return BS_OK;
 }
 
-// BS_EMB_FUSED=0: the embedding LayerNorm as its own kernel on the decode path (A/B switch).
-static bool emb_fusion_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("BS_EMB_FUSED");
-    on = !(e && *e == '0');
-  }
-  return on != 0;
-}
-
 // Enqueue one forward on `st`.  The kernels read each row's past_len from past_dev (device [B],
 // written ahead of the forward or of the graph replay); `pasts` is the host copy (profiling bytes).
 static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, void* out, float* logits, hipStream_t st,
@@ -939,7 +1035,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
   const float* cur = nullptr;
   const int* ids = nullptr;
   // bf16 decode of <= 2 rows: the embedding gather and its LayerNorm run in layer 0's LN + QKV kernel
-  const bool emb_fused = d.is_first && s->bf16 && !s->q8 && M <= 2 && s->L > 0 && emb_fusion_enabled();
+  const bool emb_fused = d.is_first && s->bf16 && !s->q8 && M <= 2 && s->L > 0;
   if (d.is_first) {
     ids = (const int*)in;
     if (host_io) {
@@ -982,7 +1078,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     // a split decode context merges in the dense GEMV's prologue when that kernel can take it
     const int nsplit = S == 1 ? attention_decode_splits(B, nh, s->max_chunks) : 1;
     a.defer_merge = s->bf16 && nsplit > 1 &&
-                    (w.sc[T_DENSE_W] ? q8_parts_enabled() && linear_q8_parts_supported(M, h, hd, nsplit)
+                    (w.sc[T_DENSE_W] ? linear_q8_parts_supported(M, h, hd, nsplit)
                                      : linear_parts_supported(M, h, hd, nsplit));
     {
       ProfScope p(s, st, 3, ctx_sum * nh * hd * 2 * s->esz);
@@ -1132,8 +1228,10 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
 
   // Decode steps on device buffers replay a captured hipGraph: the kernels read past_len from
   // device memory, set by one small kernel ahead of the replay -- unless the last forward (a last
-  // stage's, whose token pick advances past_dev by its seq) already left exactly these values there.
-  const bool past_matches = s->past_next_valid && (int)s->past_next.size() == B &&
+  // stage's, whose token pick advances past_dev by its seq) already left exactly these values there,
+  // on this same stream: a forward on another stream is not ordered behind that advance, so it always
+  // writes its own positions.
+  const bool past_matches = s->past_next_valid && s->past_stream == st && (int)s->past_next.size() == B &&
                             std::equal(pasts.begin(), pasts.end(), s->past_next.begin());
   s->past_next_valid = false;  // until this forward is enqueued
   const bool graph = S == 1 && !host_io && s->prof.cls == 0 && graphs_enabled();
@@ -1171,6 +1269,7 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
     s->past_next.assign(pasts.begin(), pasts.end());
     for (int& p : s->past_next) p += S;
     s->past_next_valid = true;
+    s->past_stream = st;
   }
   if (host_io) HIP_TRY(hipStreamSynchronize(st));
   return BS_OK;

@@ -12,9 +12,11 @@ Counterpart of the reference's per-device runtime (SURVEY.md §3.3 / §8a rows A
                   micro-batches, each owning its own KV slots, so stage s computes micro-batch
                   j while stage s+1 computes j-1 and the hops overlap compute.
 The schedule per rank is a static loop; every send/recv is posted in the same order on both
-peers, so the pattern is deadlock free.  All P2P waits are stream-level (no host blocking on
-RCCL), so the host enqueues ahead and the GPU stays busy.
+peers (DESIGN.md section 6 "Why the schedule cannot deadlock"), and every point-to-point pair is
+connected in one global order before the first round (`connect_p2p`).  All P2P waits are
+stream-level (no host blocking on RCCL), so the host enqueues ahead and the GPU stays busy.
 """
+import datetime
 import os
 import time
 
@@ -140,14 +142,25 @@ class Pipeline:
         if record is not None:
             record[j].append(self.tok[j].clone())
 
-    def step(self, seq, prompt=None, record=None, feed=None, pasts=None):
+    def _forward(self, inp, out, seq, slot, j, timing):
+        if timing is None:
+            self.ex.forward(inp, out, self.mb, seq, slot, self.past[j])
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        self.ex.forward(inp, out, self.mb, seq, slot, self.past[j])
+        e1.record()
+        timing.append((e0, e1))
+
+    def step(self, seq, prompt=None, record=None, feed=None, pasts=None, timing=None):
         """One pipeline round: every micro-batch advances by `seq` tokens (seq = prompt length
         on the prefill round, 1 on decode rounds).  `prompt` [n_mb*mb, seq] int32 on rank 0
         for the prefill round; rank 0 appends the tokens it receives to `record`.
         Continuous batching (serve.py): `pasts[j]` = every row's own position this round (all
         ranks, the same schedule); `feed[j]` = (tokens, mask) int32/bool [mb] on rank 0's device:
         rows with mask set take `tokens` (a prompt token, or a new sample's first token) instead of
-        the token the pipeline returned for them."""
+        the token the pipeline returned for them.  `timing` (a list, CUDA ranks): one event pair per
+        stage forward of this round is appended (stage busy time, bench_pipeline's prefill overlap)."""
         n_el = self.mb * seq * self.h
         for j in range(self.n_mb):
             slot = j * self.mb
@@ -167,14 +180,14 @@ class Pipeline:
                 inp = self.hin[j][:n_el]
                 _recv(inp, self.rank - 1)
             if self.is_last and not self.head_split:
-                self.ex.forward(inp, self.tok[j], self.mb, seq, slot, self.past[j])
+                self._forward(inp, self.tok[j], seq, slot, j, timing)
                 if self.world > 1:
                     self.pending[j].append(dist.isend(self.tok[j], dst=0, group=self.tok_group))
                 elif record is not None:
                     record[j].append(self.tok[j].clone())
             else:
                 out = self.hout[j][:n_el]
-                self.ex.forward(inp, out, self.mb, seq, slot, self.past[j])
+                self._forward(inp, out, seq, slot, j, timing)
                 if not self.is_last:
                     self.pending[j].append(dist.isend(out, dst=self.rank + 1))
                 else:  # head_split: open the head ring with ln_f and this rank's slice
@@ -223,21 +236,62 @@ def generate(pipe: Pipeline, prompt, steps, prompt_len):
     return torch.cat([torch.stack(r, 1) for r in rec], 0)
 
 
-def init_distributed(backend=None):
-    """Read RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* (torchrun) and initialise the process group."""
+def init_distributed(backend=None, timeout_s=None):
+    """Read RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* (torchrun) and initialise the process group.  Every
+    collective and point-to-point wait is bounded by `timeout_s` (env BS_PIPELINE_TIMEOUT_S, default
+    600 s): a schedule that stalls fails with an error instead of hanging the node."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("BS_PIPELINE_TIMEOUT_S", "600"))
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":
         torch.cuda.set_device(local)
     if not dist.is_initialized():
         kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
-        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return rank, world, local
+
+
+def p2p_edges(world, head_split):
+    """Every directed point-to-point edge the schedule uses, as (group name, src, dst), in one global order:
+    hidden states r -> r+1 ("hidden"), the head ring N-1 -> 0 -> 1 -> ... -> N-2 ("head", a chain that ends
+    at the closer N-2: no edge closes the cycle), tokens back to rank 0 ("tok", from the closer or from the
+    last rank)."""
+    if world <= 1:
+        return []
+    e = [("hidden", r, r + 1) for r in range(world - 1)]
+    if head_split:
+        closer = world - 2
+        ring = [world - 1] + list(range(0, closer + 1))
+        e += [("head", a, b) for a, b in zip(ring, ring[1:])]
+        if closer != 0:
+            e.append(("tok", closer, 0))
+    else:
+        e.append(("tok", world - 1, 0))
+    return e
+
+
+def connect_p2p(rank, world, head_split, groups, device):
+    """Open every point-to-point connection of the schedule before the first round, one edge at a time in
+    p2p_edges' global order, each a blocking 1-element exchange between its two ranks.  RCCL/NCCL connect a
+    pair lazily on its first send/recv and the host blocks there until the peer arrives; done here in one
+    order that every rank follows, the earliest unfinished edge always has both its ranks waiting on it, so
+    the exchanges complete (deadlock-free), and the timed rounds never block the host on a connection."""
+    buf = torch.zeros(1, dtype=torch.int32, device=device)
+    for name, a, b in p2p_edges(world, head_split):
+        g = groups[name]
+        if rank == a:
+            dist.send(buf, dst=b, group=g)
+        elif rank == b:
+            dist.recv(buf, src=a, group=g)
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
 
 
 def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb_rows=1, n_mb=None, max_ctx=1024,
@@ -270,6 +324,7 @@ def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb
     if world > 1:
         tok_group = dist.new_group(ranks=list(range(world)))
         head_group = dist.new_group(ranks=list(range(world)))
+        connect_p2p(rank, world, head_split, {"hidden": None, "head": head_group, "tok": tok_group}, device)
     act = torch.bfloat16 if dtype == "bf16" else torch.float32
     pipe = Pipeline(ex, rank=rank, world=world, hidden=model.hidden, mb_rows=mb_rows, n_mb=n_mb, device=device,
                     is_first=is_first, is_last=is_last, tok_group=tok_group, head_group=head_group,
@@ -286,22 +341,21 @@ def _stage_step_bytes(model, lb, le, rows, ctx, first, last, hslice, w_bytes, kv
     return b
 
 
-def bench_pipeline(args):
-    """bench.py --gpus N under torchrun: N stages, n_mb micro-batches of `batch` rows in flight.
-    Rank 0 returns the JSON dict (with per-stage roofline / HBM figures gathered from every rank) and
-    the stage ranges (for the host-CPU baseline of the same split)."""
-    rank, world, local = init_distributed("nccl")
-    dev = torch.device("cuda", local)
-    model = config.get(args.model)
-    if getattr(args, "weights", "bf16") == "int8":
-        model = config.get(model.name if model.int8_weights else model.name + "-int8")
-    B, P, K, W = args.batch, args.prompt, args.steps, args.warmup
-    prof_rounds = 0 if getattr(args, "no_profile", False) else 8
-    head_split = not getattr(args, "no_head_split", False)
-    pipe, (lb, le) = build_rank(model, rank, world, dev, dtype=args.dtype, mb_rows=B,
+def _max_over_ranks(x, dev):
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def run_pipeline(args, model, rank, world, dev, *, mb_rows, n_mb, head_split, prof_rounds):
+    """One pipeline measurement: a timed P-token prefill round (with per-stage forward events), W warm-up
+    and K timed decode rounds (barrier + sync on both sides, max over ranks), then `prof_rounds` eager
+    rounds with HIP events around every decode weight GEMV.  Collective; rank 0 returns the dict."""
+    B, P, K, W = mb_rows, args.prompt, args.steps, args.warmup
+    pipe, (lb, le) = build_rank(model, rank, world, dev, dtype=args.dtype, mb_rows=B, n_mb=n_mb,
                                 max_ctx=P + W + K + prof_rounds + 2, max_seq=P, seed=args.seed, head_split=head_split)
-    n_mb = pipe.n_mb
     cs = torch.cuda.Stream()  # a real stream: decode steps are captured as hipGraphs
+    prev = torch.cuda.current_stream()
     torch.cuda.set_stream(cs)
     prompt = None
     if rank == 0:
@@ -309,13 +363,17 @@ def bench_pipeline(args):
         prompt = torch.from_numpy(prompt_ids(1234, B * n_mb, P, model.vocab)).to(dev)
     dist.barrier()
     torch.cuda.synchronize()
+    # prefill round (the micro-batches stream through the stages: configs[3]'s overlap)
+    timing = []
     t0 = time.perf_counter()
-    pipe.step(P, prompt=prompt)
+    pipe.step(P, prompt=prompt, timing=timing)
+    torch.cuda.synchronize()
+    t_pre = time.perf_counter() - t0
+    busy_ms = sum(a.elapsed_time(b) for a, b in timing)
+    t_pre = _max_over_ranks(t_pre, dev)
     for _ in range(W):
         pipe.step(1)
     torch.cuda.synchronize()
-    dist.barrier()
-    t_prefill_warm = time.perf_counter() - t0
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -324,9 +382,7 @@ def bench_pipeline(args):
     pipe.finish()
     torch.cuda.synchronize()
     dist.barrier()
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    dt = float(dt.item())
+    dt = _max_over_ranks(time.perf_counter() - t0, dev)
     t_round = dt / K
     # per-stage roofline: eager rounds with HIP events around every decode weight GEMV of this stage
     st = pipe.ex.stage if hasattr(pipe.ex, "stage") else None
@@ -347,49 +403,102 @@ def bench_pipeline(args):
                                    hslice, w_b, w_b)
     if model.int8_weights:
         step_bytes -= (le - lb) * (12.0 * model.hidden * model.hidden * 1 - 9.0 * model.hidden * 4)
+    pre_flops = config.prefill_flops(model, le - lb, B * n_mb, P, False)
     mine = {"rank": rank, "layers": [lb, le], "head_slice": list(hslice) if hslice else None,
             "algo_bytes_per_forward": step_bytes,
-            "achieved_GBps": n_mb * step_bytes / t_round / 1e9}
+            "achieved_GBps": n_mb * step_bytes / t_round / 1e9,
+            "prefill": {"busy_ms": busy_ms, "busy_frac": busy_ms / (t_pre * 1e3),
+                        "stage_TFLOPs": pre_flops / (busy_ms * 1e-3) / 1e12 if busy_ms > 0 else None}}
     mine["frac_of_peak"] = mine["achieved_GBps"] / 8000.0
     if g is not None and g[1]:
         ms, n, byts = g
         mine["gemv"] = {"launches": n, "avg_us": ms / n * 1e3, "achieved_GBps": (byts / n) / (ms / n * 1e-3) / 1e9}
     allst = [None] * world
     dist.all_gather_object(allst, mine)
-    per_stage = [b - a for a, b in stage_ranges(world, model.n_layer)]
-    res = None
-    if rank == 0:
-        toks = B * n_mb * K
-        gemv = [x["gemv"] for x in allst if "gemv" in x]
-        res = {
-            "metric": "decode tokens/s, BLOOM pipeline", "value": toks / dt, "unit": "tokens/s", "n_gpus": world,
-            "steps": K, "warmup": W, "ms_per_step": dt * 1e3 / K, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": args.dtype,
-            "data": "synthetic: repo-generator random-init weights (seed %d), prompt ids U[0,V) seed 1234" % args.seed,
-            "config": {"workload": f"{model.name} split into {world} stages by the server's round-robin layer "
-                                   f"assignment, {n_mb} micro-batches x {B} rows in flight, RCCL send/recv"
-                                   + (", vocabulary-parallel lm_head ring" if pipe.head_split else ""),
-                       "model": model.name, "stages": world, "layers_per_stage": per_stage, "batch": B * n_mb,
-                       "micro_batch": B, "prompt": P, "parallelism": f"pp{world}",
-                       "head": "vocab-split ring" if pipe.head_split else "last stage",
-                       "hop": "fp32 hidden [mb, S, h] (the reference wire dtype; keeps the split bit-identical to one stage)"},
-            "prefill_plus_warmup_s": t_prefill_warm,
-            "per_stage": allst,
-            "stage_hbm": {"achieved_GBps_min": min(x["achieved_GBps"] for x in allst),
-                          "achieved_GBps_mean": sum(x["achieved_GBps"] for x in allst) / world,
-                          "frac_of_peak_min": min(x["frac_of_peak"] for x in allst),
-                          "frac_of_peak_mean": sum(x["frac_of_peak"] for x in allst) / world,
-                          "note": "per stage: n_mb x algorithmic bytes of one forward / time of one pipeline round"},
-        }
-        if gemv:
-            tot_t = sum(x["launches"] * x["avg_us"] for x in gemv)
-            tot_b = sum(x["launches"] * x["avg_us"] * 1e-6 * x["achieved_GBps"] * 1e9 for x in gemv)
-            ach = tot_b / (tot_t * 1e-6) / 1e9
-            res["roofline"] = {"bound": "hbm", "kernel": "gemv_rows_kernel (decode weight GEMVs of every stage)",
-                               "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0, "traffic": None,
-                               "launches": sum(x["launches"] for x in gemv), "avg_us": tot_t / sum(x["launches"] for x in gemv),
-                               "measured": f"HIP events per launch on each stage's stream, {prof_rounds} eager pipeline "
-                                           "rounds after the timed region; bytes and time summed over all stages"}
+    torch.cuda.set_stream(prev)
+    st_close = getattr(st, "close", None)
+    del pipe
+    if st_close:
+        st_close()
+    if rank != 0:
+        return None
+    toks = B * n_mb * K
+    res = {"value": toks / dt, "ms_per_step": dt * 1e3 / K, "rows": B * n_mb, "micro_batch": B, "n_mb": n_mb,
+           "head": "vocab-split ring" if head_split and world > 1 else "last stage", "per_stage": allst,
+           "stage_hbm": {"achieved_GBps_min": min(x["achieved_GBps"] for x in allst),
+                         "achieved_GBps_mean": sum(x["achieved_GBps"] for x in allst) / world,
+                         "frac_of_peak_min": min(x["frac_of_peak"] for x in allst),
+                         "frac_of_peak_mean": sum(x["frac_of_peak"] for x in allst) / world,
+                         "note": "per stage: n_mb x algorithmic bytes of one forward / time of one pipeline round"}}
+    tot_flops = config.prefill_flops(model, model.n_layer, B * n_mb, P, True)
+    res["prefill"] = {"tokens": B * n_mb * P, "ms": t_pre * 1e3, "tokens_per_s": B * n_mb * P / t_pre,
+                      "achieved_TFLOPs": tot_flops / t_pre / 1e12,
+                      "frac_of_peak": tot_flops / t_pre / 1e12 / 2500.0,
+                      "stage_busy_frac": [x["prefill"]["busy_frac"] for x in allst],
+                      "ideal_busy_frac": n_mb / (n_mb + world - 1),
+                      "note": "busy = sum of a stage's forward times (HIP events) / prefill round wall time; "
+                              "ideal = n_mb / (n_mb + stages - 1) for a perfectly overlapped fill-and-drain"}
+    gemv = [x["gemv"] for x in allst if "gemv" in x]
+    if gemv:
+        tot_t = sum(x["launches"] * x["avg_us"] for x in gemv)
+        tot_b = sum(x["launches"] * x["avg_us"] * 1e-6 * x["achieved_GBps"] * 1e9 for x in gemv)
+        ach = tot_b / (tot_t * 1e-6) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "decode weight GEMVs of every stage (gemv_rows_kernel, "
+                                                     "gemv_ldsw4_kernel)",
+                           "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0, "traffic": None,
+                           "traffic_note": "PMC passes need one rocprofv3 process per rank; collected at N = 1 only",
+                           "launches": sum(x["launches"] for x in gemv),
+                           "avg_us": tot_t / sum(x["launches"] for x in gemv),
+                           "measured": f"HIP events per launch on each stage's stream, {prof_rounds} eager pipeline "
+                                       "rounds after the timed region; bytes and time summed over all stages"}
+    return res
+
+
+def bench_pipeline(args):
+    """bench.py under torchrun (or --pipeline at N = 1): the model split into N stages, measured twice with
+    the same code -- "weak": 2N micro-batches of `batch` rows (every GPU runs 2 x n_layer / N x N = 2 x
+    n_layer layer-forwards of `batch` rows per round at every N, so per-GPU work is fixed), the line's
+    `value`; "strong": 16 x `batch` rows at every N (2N micro-batches of 8 x batch / N rows).
+    Rank 0 returns (line dict, stage ranges, model) -- the ranges for the host-CPU baseline of the split."""
+    rank, world, local = init_distributed("nccl")
+    dev = torch.device("cuda", local)
+    model = config.get(args.model)
+    if getattr(args, "weights", "bf16") == "int8":
+        model = config.get(model.name if model.int8_weights else model.name + "-int8")
+    prof_rounds = 0 if getattr(args, "no_profile", False) else 8
+    head_split = not getattr(args, "no_head_split", False)
+    n_mb = 2 * world
+    weak = run_pipeline(args, model, rank, world, dev, mb_rows=args.batch, n_mb=n_mb, head_split=head_split,
+                        prof_rounds=prof_rounds)
+    strong = None
+    if not getattr(args, "no_strong", False):
+        rows = 16 * args.batch
+        strong = run_pipeline(args, model, rank, world, dev, mb_rows=max(1, rows // n_mb), n_mb=n_mb,
+                              head_split=head_split, prof_rounds=0)
     dist.barrier()
     dist.destroy_process_group()
+    if rank != 0:
+        return None, stage_ranges(world, model.n_layer), model
+    per_stage = [b - a for a, b in stage_ranges(world, model.n_layer)]
+    res = {
+        "metric": "decode tokens/s, BLOOM pipeline", "value": weak["value"], "unit": "tokens/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": weak["ms_per_step"], "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic: repo-generator random-init weights (seed %d), prompt ids U[0,V) seed 1234" % args.seed,
+        "config": {"workload": f"{model.name} split into {world} stages by the server's round-robin layer "
+                               f"assignment, {n_mb} micro-batches x {args.batch} rows in flight, RCCL send/recv"
+                               + (", vocabulary-parallel lm_head ring" if weak["head"] == "vocab-split ring" else ""),
+                   "model": model.name, "stages": world, "layers_per_stage": per_stage, "batch": weak["rows"],
+                   "micro_batch": args.batch, "prompt": args.prompt, "parallelism": f"pp{world}",
+                   "head": weak["head"],
+                   "hop": "fp32 hidden [mb, S, h] (the reference wire dtype; keeps the split bit-identical to one stage)"},
+        "weak_definition": "2N micro-batches x batch rows: per-GPU layer-forwards per round fixed at 2 x n_layer",
+        "per_stage": weak["per_stage"], "stage_hbm": weak["stage_hbm"], "prefill": weak["prefill"],
+    }
+    if "roofline" in weak:
+        res["roofline"] = weak["roofline"]
+    if strong is not None:
+        res["strong"] = {k: strong[k] for k in ("value", "ms_per_step", "rows", "micro_batch", "n_mb", "stage_hbm",
+                                                "prefill")}
+        res["strong"]["definition"] = "16 x batch rows in flight at every N (2N micro-batches of 8 x batch / N rows)"
     return res, stage_ranges(world, model.n_layer), model

@@ -77,11 +77,11 @@ class TensorView(ctypes.Structure):
 
 
 EXPORTS = [
-    "bs_init_stage", "bs_forward", "bs_reset_kv", "bs_release", "bs_last_error", "bs_stage_info",
+    "bs_init_stage", "bs_forward", "bs_reset_kv", "bs_read_kv", "bs_release", "bs_last_error", "bs_stage_info",
     "bs_stage_weight_count", "bs_abi_version", "bs_profile_enable", "bs_profile_read",
     "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
     "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice", "bs_stream_delay", "bs_set_sampling",
-    "bs_build_id", "bs_hbm_probe", "bs_init_stage_file", "bs_weights_file_probe",
+    "bs_build_id", "bs_hbm_probe", "bs_mfma_probe", "bs_init_stage_file", "bs_weights_file_probe",
 ]
 
 _LIB = None
@@ -109,6 +109,7 @@ def lib():
         L.bs_weights_file_probe.argtypes = [ctypes.c_char_p] + [ctypes.POINTER(i32)] * 3
         L.bs_forward.argtypes = [vp, ctypes.POINTER(Step), vp, vp, vp, vp]
         L.bs_reset_kv.argtypes = [vp, i32]
+        L.bs_read_kv.argtypes = [vp, i32, i32, i32, i32, vp]
         L.bs_release.argtypes = [vp]
         L.bs_release.restype = None
         L.bs_last_error.restype = ctypes.c_char_p
@@ -133,6 +134,7 @@ def lib():
         L.bs_head_slice.argtypes = [vp, vp, i32, vp, vp, vp, vp]
         L.bs_set_sampling.argtypes = [vp, i32, ctypes.c_float, ctypes.c_uint64]
         L.bs_hbm_probe.argtypes = [i32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        L.bs_mfma_probe.argtypes = [i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         _LIB = L
     return _LIB
 
@@ -271,6 +273,13 @@ class Stage:
         else:
             self.past[slot] = 0
 
+    def read_kv(self, layer, slot, pos0, npos):
+        """KV row `slot` of local layer `layer`, positions [pos0, pos0+npos): fp32 [2 (K, V)][n_head][npos][hd]."""
+        nh = self.desc.n_head
+        out = np.empty((2, nh, npos, self.hidden // nh), np.float32)
+        _check(lib().bs_read_kv(self._h, layer, slot, pos0, npos, out.ctypes.data))
+        return out
+
     def info(self):
         d = StageDesc()
         wb, kb, sb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
@@ -322,6 +331,13 @@ def hbm_probe(device=0, nbytes=2 << 30):
     r, c = ctypes.c_double(), ctypes.c_double()
     _check(lib().bs_hbm_probe(device, nbytes, ctypes.byref(r), ctypes.byref(c)))
     return r.value, c.value
+
+
+def mfma_probe(device=0):
+    """Measured dense bf16 MFMA TFLOP/s of a device (bs_mfma_probe): (32x32x16 chains, 16x16x32 chains)."""
+    a, b = ctypes.c_double(), ctypes.c_double()
+    _check(lib().bs_mfma_probe(device, ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
 
 
 def probe_weights_file(path):

@@ -129,6 +129,9 @@ int bs_init_stage_file(const bs_stage_desc *desc, const char *path, bs_stage **o
 int bs_weights_file_probe(const char *path, int32_t *hidden, int32_t *n_layer, int32_t *vocab);
 
 /* Stage forward, stream-ordered on `stream` (hipStream_t, NULL = the stage's own stream).
+ * One stage is single-producer: its forwards share the stage's workspace, so a caller that moves a
+ * stage from one stream to another must order the new stream behind the old one (an event wait);
+ * the library then re-writes every row's position on the new stream itself.
  *  in : first stage -> int32 token ids [B][S]; otherwise fp32 hidden [B][S][hidden]
  *  out: last stage  -> int32 token ids [B] (greedy argmax of each row's last position);
  *       otherwise fp32 hidden [B][S][hidden]
@@ -166,6 +169,10 @@ int bs_set_sampling(bs_stage *stage, int32_t top_k, float temperature, uint64_t 
 
 /* Forget the cached positions of one KV row (slot), or of all rows when slot < 0. */
 int bs_reset_kv(bs_stage *stage, int32_t slot);
+/* Read back KV row `slot` of the stage's local layer `layer`, positions [pos0, pos0 + npos), as fp32
+ * out[2 (K, V)][n_head][npos][head_dim].  Synchronizes the stage's own stream; the caller orders any
+ * other stream it forwarded on.  For verification (parity tests hand a device cache to the checker). */
+int bs_read_kv(const bs_stage *stage, int32_t layer, int32_t slot, int32_t pos0, int32_t npos, float *out);
 
 void bs_release(bs_stage *stage);
 
@@ -204,6 +211,10 @@ int bs_stream_delay(void *stream, int32_t microseconds);
 /* Measurement aid (bench.py "hbm_measured"): STREAM-like HBM rates of a device, best of 10 runs over
  * `bytes` (a multiple of 1 MiB) -- read: non-temporal 16-B loads; copy: read + write bytes / time. */
 int bs_hbm_probe(int32_t device, uint64_t bytes, double *read_gbps, double *copy_gbps);
+/* Measurement aid (bench.py "mfma_measured"): dense bf16 matrix-core TFLOP/s of a device, best of 5 runs of
+ * register-operand v_mfma_f32_32x32x16_bf16 / v_mfma_f32_16x16x32_bf16 chains (8 independent chains per wave,
+ * 8 waves per CU, no memory traffic).  The measured counterpart of the vendor dense peak. */
+int bs_mfma_probe(int32_t device, double *tflops_32x32x16, double *tflops_16x16x32);
 
 /* ---- Reference wire codec (utils.cpp:124-368): size_t n; per tensor {int32 dtype,
  * size_t ndim, int64 dims[ndim], raw little-endian data}. size_t is 8 bytes (LP64). ---- */

@@ -395,4 +395,18 @@ int or_read_kv(const or_stage *s, int li, int which, int row, int head, int pos,
   return 0;
 }
 
+/* Test infrastructure: overwrite KV row `row` of local layer li, positions [pos0, pos0+npos), from
+ * in[2 (K, V)][nh][npos][hd] (a device cache read back through bs_read_kv), so a decode step at a long
+ * context can be checked without the checker recomputing every earlier position. */
+int or_write_kv(or_stage *s, int li, int row, int pos0, int npos, const float *in) {
+  if (li < 0 || li >= s->le - s->lb || row < 0 || row >= s->max_batch || pos0 < 0 || npos < 0 ||
+      pos0 + npos > s->max_ctx)
+    return -1;
+  for (int w = 0; w < 2; w++)
+    for (int hh = 0; hh < s->nh; hh++)
+      memcpy(kv_ptr(s, li, w, row, hh, pos0), in + ((size_t)(w * s->nh + hh) * npos) * s->hd,
+             sizeof(float) * (size_t)npos * s->hd);
+  return 0;
+}
+
 int or_num_threads(void) { return omp_get_max_threads(); }

@@ -27,6 +27,8 @@ def lib():
         L.or_alibi_slopes.argtypes = [ctypes.c_int, ctypes.c_void_p]
         L.or_read_kv.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p]
         L.or_num_threads.restype = ctypes.c_int
+        L.or_write_kv.restype = ctypes.c_int
+        L.or_write_kv.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 4 + [ctypes.c_void_p]
         L.or_set_accum_double.argtypes = [ctypes.c_int]
         L.or_set_skip_round.argtypes = [ctypes.c_int]
         L.or_quantize_int8.restype = ctypes.c_int
@@ -111,6 +113,13 @@ class OracleStage:
         out = np.empty(head_dim, dtype=np.float32)
         lib().or_read_kv(self.h, layer_local, which, row, head, pos, _p(out))
         return out
+
+    def write_kv(self, layer_local, row, pos0, kv):
+        """Overwrite KV row `row` of local layer `layer_local` from kv fp32 [2][n_head][npos][hd] (e.g. a
+        device cache read back with Stage.read_kv)."""
+        kv = np.ascontiguousarray(kv, dtype=np.float32)
+        if lib().or_write_kv(self.h, layer_local, row, pos0, kv.shape[2], _p(kv)) != 0:
+            raise ValueError("or_write_kv: range outside the stage")
 
     def close(self):
         if self.h:

@@ -1,0 +1,114 @@
+"""Parity at real bloom-7b1 / bloom-3b width for the two configurations BASELINE.json quotes on them.
+
+configs[4] -- bloom-7b1 batch-32 decode, KV growing to 2k tokens (stage forward inference.cpp:145-218 on the
+server.py:893-905 ranges): h = 4096, 32 heads (hd 128), 2 layers, a reduced vocabulary (V = 4096: the
+argmax head is then one more (4096, 4096) GEMV).  B in {16, 20, 32} rows decode by graph replay from a
+16-token prompt through contexts 256 / 512 / 1024 / 2048.  This runs the bloom-7b1 rows of the batched-GEMV
+table (kernels.hip kTileTable: (12288, 4096) T = 3, (4096, 4096) split-K at M > 16, (16384, 4096)
+gemv_ldsw4<T = 4>, (4096, 16384) split-K) and decode attention at B * heads = 512 / 640 / 1024 over up to
+2048 cached positions.
+
+The checker (oracle/bloom_oracle.c, bf16 mode) cannot afford 2000 decode steps of 32 rows at this width,
+so between checkpoints the device runs free (its own argmax tokens) and at each checkpoint the device
+cache written since the last one is handed to the checker (bs_read_kv -> or_write_kv); then both run the
+checkpoint step from the same token: logits max-abs <= 2e-2 (north_star), ids equal unless the checker's
+top-2 margin is < 2e-2, and the K/V rows the step appends (the device's QKV epilogue vs the checker's
+projection) within the wide-block hidden-state bound.  The prompt's cache is the checker's own and is
+compared with the device's the same way.
+
+configs[3] -- bloom-7b1 micro-batched prefill: a 512-token prefill of B = 2 rows at hd = 128 (h = 4096) and
+hd = 80 (h = 2560, bloom-3b), one layer: eight 64-query tiles under the causal mask, so the MFMA flash
+attention (attn_prefill_mfma_kernel) walks up to eight 64-key tiles per query tile; then one decode step
+over the 512 cached positions.
+"""
+import numpy as np
+import pytest
+
+from distributed_inference_demo_amd.stage import Stage
+from oracle import gen_np
+from oracle.oracle import OracleStage
+
+from test_gpu_parity import assert_ids_match, check_close, check_logits
+
+pytestmark = pytest.mark.gpu
+
+
+def _kv_rows(o, layer, row, pos, nh, hd):
+    """The checker's K/V at one position: [2][nh][1][hd]."""
+    return np.stack([np.stack([o.read_kv(layer, w, row, hh, pos, hd) for hh in range(nh)])[:, None, :]
+                     for w in range(2)])
+
+
+@pytest.mark.parametrize("B", [16, 20, 32])
+def test_bloom7b1_width_batched_graph_decode_to_ctx2048(B):
+    import torch
+    h, nh, L, V, P = 4096, 32, 2, 4096, 16
+    hd = h // nh
+    checkpoints = (256, 512, 1024, 2048)
+    max_ctx = checkpoints[-1] + 1
+    gs = Stage(h, nh, L, V, 0, L, dtype="bf16", max_batch=B, max_ctx=max_ctx, max_tokens=B * P, seed=51)
+    os_ = OracleStage(h, nh, L, V, 0, L, bf16=True, max_batch=B, max_ctx=max_ctx, seed=51)
+    ids = gen_np.prompt_ids(57, B, P, V).astype(np.int32)
+    dev = torch.device("cuda", 0)
+    cs = torch.cuda.Stream()
+    with torch.cuda.stream(cs):
+        tin = torch.from_numpy(ids).to(dev)
+        tok = torch.empty(B, dtype=torch.int32, device=dev)
+        lg = torch.empty((B, V), dtype=torch.float32, device=dev)
+        gs.forward(tin, tok, B, P, slot=0, past_len=0, logits=lg, stream=cs.cuda_stream)
+        to, lo = os_.forward(ids, B, P, want_logits=True)
+        cs.synchronize()
+        check_logits(lg.cpu().numpy(), lo, "bf16", f"B={B} prefill")
+        assert_ids_match(tok.cpu().numpy(), to, lo, f"B={B} prefill")
+        for layer in range(L):  # the prompt's cache: device prefill epilogue vs the checker
+            for r in (0, B // 2, B - 1):
+                ref = np.concatenate([_kv_rows(os_, layer, r, p, nh, hd) for p in range(P)], axis=2)
+                check_close(gs.read_kv(layer, r, 0, P), ref, "bf16", f"B={B} prefill KV layer {layer} row {r}")
+        tok.copy_(torch.from_numpy(to))
+        past = synced = P
+        for ctx in checkpoints:
+            while past < ctx - 1:  # free-running graph replays: the device feeds back its own tokens
+                gs.forward(tok, tok, B, 1, slot=0, past_len=past, stream=cs.cuda_stream)
+                past += 1
+            cs.synchronize()
+            for layer in range(L):  # hand the device cache written since the last checkpoint to the checker
+                for r in range(B):
+                    os_.write_kv(layer, r, synced, gs.read_kv(layer, r, synced, past - synced))
+            t_in = tok.cpu().numpy()
+            gs.forward(tok, tok, B, 1, slot=0, past_len=past, logits=lg, stream=cs.cuda_stream)
+            to, lo = os_.forward(t_in.reshape(B, 1), B, 1, past_len=past, want_logits=True)
+            cs.synchronize()
+            err = check_logits(lg.cpu().numpy(), lo, "bf16", f"B={B} decode at ctx {ctx}")
+            assert_ids_match(tok.cpu().numpy(), to, lo, f"B={B} decode at ctx {ctx}")
+            for layer in range(L):  # the position this step appended: device QKV epilogue vs the checker
+                for r in (0, B - 1):
+                    check_close(gs.read_kv(layer, r, past, 1), _kv_rows(os_, layer, r, past, nh, hd), "bf16",
+                                f"B={B} ctx {ctx} new KV layer {layer} row {r}")
+            print(f"B={B} ctx {ctx}: logits max-abs {err:.3e}")
+            past += 1
+            synced = past  # the checker computed this position itself
+    gs.close()
+    os_.close()
+
+
+@pytest.mark.parametrize("h,nh", [(4096, 32), (2560, 32)])
+def test_prefill512_multitile_causal_attention_wide_heads(h, nh):
+    """configs[3] micro-batch shape: B = 2 rows x 512 tokens through one layer (hd 128 / 80), then one decode
+    step over the 512 cached positions; hidden states within the wide-block bound."""
+    B, S, V = 2, 512, 1024
+    gs = Stage(h, nh, 1, V, 0, 1, dtype="bf16", max_batch=B, max_ctx=S + 1, max_tokens=B * S, seed=61,
+               is_last=False)
+    os_ = OracleStage(h, nh, 1, V, 0, 1, bf16=True, max_batch=B, max_ctx=S + 1, seed=61, is_last=False)
+    ids = gen_np.prompt_ids(63, B, S + 1, V).astype(np.int32)
+    out_g = gs.forward_host(ids[:, :S], B, S, past_len=0)
+    out_o = os_.forward(ids[:, :S], B, S, past_len=0)
+    err = check_close(out_g, out_o, "bf16", f"h={h} prefill {B}x{S}")
+    # per 64-query tile: the causal tiles see 1..8 key tiles
+    for t in range(0, S, 64):
+        check_close(out_g[:, t:t + 64], out_o[:, t:t + 64], "bf16", f"h={h} query tile {t // 64}")
+    d_g = gs.forward_host(ids[:, S:S + 1], B, 1, past_len=S)
+    d_o = os_.forward(ids[:, S:S + 1], B, 1, past_len=S)
+    err1 = check_close(d_g, d_o, "bf16", f"h={h} decode at ctx {S + 1}")
+    print(f"h={h} hd={h // nh}: prefill max-abs {err:.3e}, decode {err1:.3e}")
+    gs.close()
+    os_.close()

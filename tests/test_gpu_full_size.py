@@ -4,8 +4,9 @@
 Reference tail these pin: run_inference_with_decoding (inference.cpp:272-327) and the tail JNI
 entry (native-lib.cpp:1368-1443) -- here the greedy pick of the full V = 250880 vocabulary.
 
-  * bloom-1b1, all 24 layers, V = 250880, B = 1: a 512-token prefill, then 16 graph-replayed decode
-    steps on device buffers (teacher-forced with the checker's tokens).  bf16 mode against the
+  * bloom-1b1, all 24 layers, V = 250880, B = 1: a 512-token prefill, then 128 graph-replayed decode
+    steps on device buffers (north_star's fixed 128-token decode; teacher-forced with the checker's tokens,
+    so every step compares logits from the same inputs).  bf16 mode against the
     bf16-mode checker (same storage roundings): the greedy id equal to the checker's unless the
     checker's own top-2 margin is < 2e-2 (north_star's id criterion); logits mean-abs <= 4e-3 and
     max-abs <= 2.5e-2.  The max bound is above north_star's example 2e-2 at this depth because the
@@ -34,7 +35,7 @@ BF16_FULL_MEAN_TOL = 4e-3    # logits mean-abs, full depth
 def test_bloom1b1_full_prefill512_then_graph_decode_bf16():
     import torch
     m = config.get("bloom-1b1")
-    P, STEPS = 512, 16
+    P, STEPS = 512, 128
     g = Stage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, m.n_layer, dtype="bf16", max_batch=1,
               max_ctx=P + STEPS + 1, max_tokens=P, seed=0)
     o = OracleStage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, m.n_layer, bf16=True, max_batch=1,
@@ -42,7 +43,7 @@ def test_bloom1b1_full_prefill512_then_graph_decode_bf16():
     ids = prompt_ids(1234, 1, P, m.vocab)
     dev = torch.device("cuda", 0)
     cs = torch.cuda.Stream()
-    errs, means = [], []
+    errs, means, same = [], [], 0
     with torch.cuda.stream(cs):
         tin = torch.from_numpy(ids).to(dev)
         tok = torch.empty(1, dtype=torch.int32, device=dev)
@@ -63,7 +64,9 @@ def test_bloom1b1_full_prefill512_then_graph_decode_bf16():
             errs.append(float(np.abs(gl - lo).max()))
             means.append(float(np.abs(gl - lo).mean()))
             assert_ids_match(gt, to, lo, f"decode step {step}")
-    print(f"bloom-1b1 full: logits max-abs prefill {errs[0]:.3e}, decode {['%.3e' % e for e in errs[1:]]}, "
+            same += int(gt[0] == to[0])
+    print(f"bloom-1b1 full: {same}/{STEPS} decode ids identical to the checker's (the rest are top-2 ties < 2e-2); "
+          f" logits max-abs prefill {errs[0]:.3e}, decode max {max(errs[1:]):.3e} median {float(np.median(errs[1:])):.3e}, "
           f"max |logit| {float(np.abs(lo).max()):.2f}, mean-abs {max(means):.2e}")
     assert max(means) <= BF16_FULL_MEAN_TOL, means
     assert max(errs) <= BF16_FULL_TOL, errs

@@ -139,3 +139,57 @@ def test_3b_uneven_four_stage_split_bf16_teacher_forced():
             assert top2[1] - top2[0] < BF16_TOL, f"step {i} row {b}: {got[b, i]} != {want[b]}, top-2 {top2}"
         if i < STEPS:  # the checker continues on the pipeline's own tokens
             _, lo = ref.forward(got[:, i].reshape(B, 1).astype(np.int32), B, 1, past_len=P + i, want_logits=True)
+
+
+_NCCL_WORLD1 = r"""
+import os, sys
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.getcwd())
+from distributed_inference_demo_amd import config
+from distributed_inference_demo_amd.pipeline import build_rank, generate, init_distributed
+from distributed_inference_demo_amd.stage import prompt_ids
+rank, world, local = init_distributed("nccl", timeout_s=120)
+assert (rank, world, dist.get_backend()) == (0, 1, "nccl")
+m = config.BloomDims("tinygpu", 256, 2, 4, vocab=1024)
+dev = torch.device("cuda", 0)
+pipe, rng = build_rank(m, 0, 1, dev, dtype=sys.argv[2], mb_rows=2, n_mb=2, max_ctx=40, max_seq=8, seed=11)
+assert rng == (0, 2) and type(pipe.ex).__name__ == "StageExecutor"
+cs = torch.cuda.Stream()
+torch.cuda.set_stream(cs)
+prompt = torch.from_numpy(prompt_ids(1234, 4, 8, m.vocab)).to(dev)
+toks = generate(pipe, prompt, 12, 8)
+np.save(sys.argv[1], toks.cpu().numpy())
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_pipeline_nccl_world1_stage_executor_graph_decode(dtype, tmp_path):
+    """The product pipeline path end to end on one GPU: init_distributed("nccl") (an RCCL world-1 group
+    with a timeout), build_rank -> a libbloomstage Stage behind StageExecutor, 2 micro-batches of 2 rows
+    whose decode steps replay captured hipGraphs on device buffers.  fp32: greedy ids identical to the
+    single-stage checker; bf16: every id the bf16 checker's argmax on the pipeline's own prefix unless the
+    checker's top-2 margin is < 2e-2."""
+    import subprocess
+    import sys
+    out = str(tmp_path / "toks.npy")
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run([sys.executable, "-c", _NCCL_WORLD1, out, dtype], check=True, env=env, cwd=root, timeout=180)
+    got = np.load(out)
+    B, steps = 4, 12
+    assert got.shape == (B, steps + 1)
+    ref = OracleStage(256, 4, 2, 1024, 0, 2, bf16=(dtype == "bf16"), max_batch=B, max_ctx=40, seed=11)
+    tok, lo = ref.forward(prompt_ids(1234, B, 8, 1024), B, 8, want_logits=True)
+    for i in range(steps + 1):
+        if dtype == "fp32":
+            assert np.array_equal(got[:, i], tok), (i, got[:, i], tok)
+        else:
+            for b in np.flatnonzero(got[:, i] != lo.argmax(1)):
+                top2 = np.sort(lo[b])[-2:]
+                assert top2[1] - top2[0] < BF16_TOL, f"step {i} row {b}: top-2 {top2}"
+        if i < steps:  # the checker continues on the pipeline's own tokens
+            tok, lo = ref.forward(got[:, i].reshape(B, 1).astype(np.int32), B, 1, past_len=8 + i, want_logits=True)

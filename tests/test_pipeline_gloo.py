@@ -2,6 +2,7 @@
 states forwarded rank to rank, tokens returned tail -> head.  Each rank's stage math is the CPU
 checker (test infrastructure standing in for the GPU stage, which needs an MI355X); the test
 checks the schedule produces exactly the single-stage greedy tokens."""
+import functools
 import os
 import socket
 
@@ -16,20 +17,24 @@ from distributed_inference_demo_amd.pipeline import build_rank, generate
 from oracle.oracle import OracleStage, prompt_ids
 
 MODEL = config.BloomDims("tiny", 64, 4, 4, vocab=512)
+# 30 layers: round_robin_module_arrangement(8, 30) (server.py:893-903) gives bloom-7b1's 8-stage split
+# 4,4,4,4,4,4,3,3 (BASELINE.json configs[3])
+MODEL30 = config.BloomDims("tiny30", 64, 30, 4, vocab=512)
 SEED, P, STEPS, MB = 3, 6, 10, 2
 
 
 class OracleExecutor:
-    def __init__(self, lb, le, first, last, max_batch, max_ctx, hslice=None):
-        self.st = OracleStage(MODEL.hidden, MODEL.n_head, MODEL.n_layer, MODEL.vocab, lb, le, max_batch=max_batch,
+    def __init__(self, lb, le, first, last, max_batch, max_ctx, hslice=None, model=MODEL):
+        self.model = model
+        self.st = OracleStage(model.hidden, model.n_head, model.n_layer, model.vocab, lb, le, max_batch=max_batch,
                               max_ctx=max_ctx, seed=SEED, is_first=first, is_last=last)
         self.first, self.last, self.hslice = first, last, hslice
         if hslice is not None:  # layer-free stage owning the tied head for ln_f + the vocab slice
-            self.head = OracleStage(MODEL.hidden, MODEL.n_head, MODEL.n_layer, MODEL.vocab, 0, 0, max_batch=max_batch,
+            self.head = OracleStage(model.hidden, model.n_head, model.n_layer, model.vocab, 0, 0, max_batch=max_batch,
                                     max_ctx=max_ctx, seed=SEED, is_first=False, is_last=True)
 
     def head_norm(self, hidden, batch, seq, xn):
-        xn.copy_(torch.from_numpy(self.head.head_norm(hidden.numpy()[: batch * seq * MODEL.hidden], batch, seq).reshape(-1)))
+        xn.copy_(torch.from_numpy(self.head.head_norm(hidden.numpy()[: batch * seq * self.model.hidden], batch, seq).reshape(-1)))
 
     def head_slice(self, xn, batch, keys_in, keys_out, tokens):
         kin = None if keys_in is None else keys_in.numpy().view(np.uint64)
@@ -50,13 +55,16 @@ class OracleExecutor:
         out.copy_(torch.from_numpy(np.ascontiguousarray(y).reshape(-1)[: out.numel()]).view(out.shape))
 
 
-def _worker(rank, world, port, q, head_split=False, resume=0):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+def _worker(rank, world, port, q, head_split=False, resume=0, model=MODEL):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      OMP_NUM_THREADS="1")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        pipe, _ = build_rank(MODEL, rank, world, torch.device("cpu"), mb_rows=MB, max_ctx=P + STEPS + resume + 2,
-                             max_seq=P, executor_factory=OracleExecutor, head_split=head_split, dtype="fp32")
-        prompt = torch.from_numpy(prompt_ids(1234, MB * pipe.n_mb, P, MODEL.vocab)) if rank == 0 else None
+        pipe, rng = build_rank(model, rank, world, torch.device("cpu"), mb_rows=MB, max_ctx=P + STEPS + resume + 2,
+                               max_seq=P, executor_factory=functools.partial(OracleExecutor, model=model),
+                               head_split=head_split, dtype="fp32")
+        q.put(("range", rank, rng, pipe.n_mb))
+        prompt = torch.from_numpy(prompt_ids(1234, MB * pipe.n_mb, P, model.vocab)) if rank == 0 else None
         toks = generate(pipe, prompt, STEPS, P)
         if resume:  # rounds after finish() continue from the tokens finish() collected
             rec = [[] for _ in range(pipe.n_mb)] if rank == 0 else None
@@ -66,7 +74,7 @@ def _worker(rank, world, port, q, head_split=False, resume=0):
             if rank == 0:
                 toks = torch.cat([toks, torch.cat([torch.stack(r, 1) for r in rec], 0)], 1)
         if rank == 0:
-            q.put(toks.numpy())
+            q.put(("tokens", toks.numpy()))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -80,19 +88,53 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,head_split,resume", [(2, False, 0), (3, False, 0), (2, True, 0), (3, True, 0),
-                                                     (4, True, 0), (2, False, 3), (3, True, 3)])
-def test_pipeline_matches_single_stage(world, head_split, resume):
+def _run(world, head_split, resume, model=MODEL):
+    """Spawn `world` gloo ranks; returns (rank 0's tokens, {rank: (layer range, micro-batches)})."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, head_split, resume)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, head_split, resume, model)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got, ranges = None, {}
+    while got is None or len(ranges) < world:
+        msg = q.get(timeout=180)
+        if msg[0] == "tokens":
+            got = msg[1]
+        else:
+            ranges[msg[1]] = (tuple(msg[2]), msg[3])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return got, ranges
+
+
+def _single_stage(model, B, steps):
+    ref = OracleStage(model.hidden, model.n_head, model.n_layer, model.vocab, 0, model.n_layer, max_batch=B,
+                      max_ctx=P + steps + 2, seed=SEED)
+    tok = ref.forward(prompt_ids(1234, B, P, model.vocab), B, P)
+    want = [tok]
+    for i in range(steps):
+        tok = ref.forward(tok.reshape(B, 1), B, 1, past_len=P + i)
+        want.append(tok)
+    return np.stack(want, 1)
+
+
+def test_pipeline_eight_stages_bloom7b1_split():
+    """BASELINE.json configs[3]'s shape on 8 gloo ranks: 30 layers split 4,4,4,4,4,4,3,3 by the server's
+    round-robin assignment, 16 micro-batches in flight, the vocabulary-parallel head as an 8-slice ring;
+    the greedy ids equal one stage's."""
+    got, ranges = _run(8, True, 0, MODEL30)
+    assert [ranges[r][0][1] - ranges[r][0][0] for r in range(8)] == [4, 4, 4, 4, 4, 4, 3, 3]
+    assert all(ranges[r][1] == 16 for r in range(8))
+    assert got.shape[0] == MB * 16
+    assert np.array_equal(got, _single_stage(MODEL30, got.shape[0], STEPS))
+
+
+@pytest.mark.parametrize("world,head_split,resume", [(2, False, 0), (3, False, 0), (2, True, 0), (3, True, 0),
+                                                     (4, True, 0), (2, False, 3), (3, True, 3)])
+def test_pipeline_matches_single_stage(world, head_split, resume):
+    got, _ = _run(world, head_split, resume)
     # single stage reference, all rows at once
     B = got.shape[0]
     assert B == MB * world * (2 if head_split else 1)
