@@ -363,6 +363,11 @@ def _pipeline_n1(args):
 
 def main():
     args = parse()
+    # the driver reads ONE JSON line from stdout: libraries that print banners there (RCCL prints its version
+    # block when a communicator is created) are sent to stderr at the file-descriptor level
+    out_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     ranges = model = None
     if world > 1 or args.gpus > 1 or args.pipeline:
@@ -385,8 +390,9 @@ def main():
         model = config.get(args.model)
     if res is not None and args.cpu_baseline:  # rank 0, after the process group is gone
         res["cpu_baseline"] = cpu_baseline(model, args.cpu_steps, args.seed, ranges=ranges)
+    sys.stdout.flush()
     if res is not None:
-        print(json.dumps(res), flush=True)
+        os.write(out_fd, (json.dumps(res) + "\n").encode())
 
 
 if __name__ == "__main__":
