@@ -15,7 +15,9 @@ checkpoint step from the same token: ids equal unless the checker's top-2 margin
 the wide-width bound (max-abs <= 2.5e-2, mean-abs <= 4e-3: the rule test_gpu_full_size.py states for full
 depth -- at h = 4096 one rounding flip of an intermediate moves a logit 1.6x as far as at h = 1536, and the
 first device run measured 0.0216 max at the prefill, the same bf16 flip noise), and the K/V rows the step
-appends (the device's QKV epilogue vs the checker's projection) within the wide-block hidden-state bound.  The prompt's cache is the checker's own and is
+appends (the device's QKV epilogue vs the checker's projection) within the wide-block hidden-state bound plus
+one bf16 storage ulp (check_bf16_stored: cached values are rounded to bf16, and two correct paths may round a
+value in [4, 8) to neighbours 0.03125 apart).  The prompt's cache is the checker's own and is
 compared with the device's the same way.
 
 configs[3] -- bloom-7b1 micro-batched prefill: a 512-token prefill of B = 2 rows at hd = 128 (h = 4096) and
@@ -30,7 +32,7 @@ from distributed_inference_demo_amd.stage import Stage
 from oracle import gen_np
 from oracle.oracle import OracleStage
 
-from test_gpu_parity import assert_ids_match, check_close
+from test_gpu_parity import assert_ids_match, check_bf16_stored, check_close
 
 WIDE_LOGIT_TOL, WIDE_LOGIT_MEAN_TOL = 2.5e-2, 4e-3
 
@@ -73,7 +75,7 @@ def test_bloom7b1_width_batched_graph_decode_to_ctx2048(B):
         for layer in range(L):  # the prompt's cache: device prefill epilogue vs the checker
             for r in (0, B // 2, B - 1):
                 ref = np.concatenate([_kv_rows(os_, layer, r, p, nh, hd) for p in range(P)], axis=2)
-                check_close(gs.read_kv(layer, r, 0, P), ref, "bf16", f"B={B} prefill KV layer {layer} row {r}")
+                check_bf16_stored(gs.read_kv(layer, r, 0, P), ref, f"B={B} prefill KV layer {layer} row {r}")
         tok.copy_(torch.from_numpy(to))
         past = synced = P
         for ctx in checkpoints:
@@ -92,8 +94,8 @@ def test_bloom7b1_width_batched_graph_decode_to_ctx2048(B):
             assert_ids_match(tok.cpu().numpy(), to, lo, f"B={B} decode at ctx {ctx}")
             for layer in range(L):  # the position this step appended: device QKV epilogue vs the checker
                 for r in (0, B - 1):
-                    check_close(gs.read_kv(layer, r, past, 1), _kv_rows(os_, layer, r, past, nh, hd), "bf16",
-                                f"B={B} ctx {ctx} new KV layer {layer} row {r}")
+                    check_bf16_stored(gs.read_kv(layer, r, past, 1), _kv_rows(os_, layer, r, past, nh, hd),
+                                      f"B={B} ctx {ctx} new KV layer {layer} row {r}")
             print(f"B={B} ctx {ctx}: logits max-abs {err:.3e}")
             past += 1
             synced = past  # the checker computed this position itself
