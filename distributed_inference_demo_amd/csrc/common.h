@@ -59,6 +59,23 @@ __device__ __forceinline__ float gelu_bloom(float x) {
   return x * 0.5f * (1.0f + tanhf(0.79788456f * x * (1.0f + 0.044715f * x * x)));
 }
 
+// Weight loads (NT: non-temporal) and an 8-wide bf16 dot product on v_dot2c_f32_bf16.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+template <int NT>
+__device__ __forceinline__ bf16x8 wload(const bf16* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
+  else return *reinterpret_cast<const bf16x8*>(p);
+}
+
+__device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float acc) {
+  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[0], a[1]}, (bf16x2){b[0], b[1]}, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[2], a[3]}, (bf16x2){b[2], b[3]}, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[4], a[5]}, (bf16x2){b[4], b[5]}, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[6], a[7]}, (bf16x2){b[6], b[7]}, acc, false);
+  return acc;
+}
+
 // Monotone float -> uint32 key (larger float => larger key).
 __device__ __forceinline__ uint32_t f32_order_key(float f) {
   uint32_t u = __float_as_uint(f);

@@ -465,21 +465,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_mfma_kernel(const bf16* __res
 // per lane are reduced across the wave at the end.  Small blocks (4 waves) and one wave per
 // 1-4 rows give every CU several blocks, so no wave-quantisation tail on N = h GEMVs.
 // ------------------------------------------------------------------------------------
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-
-template <int NT>
-__device__ __forceinline__ bf16x8 wload(const bf16* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
-  else return *reinterpret_cast<const bf16x8*>(p);
-}
-
-__device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float acc) {
-  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[0], a[1]}, (bf16x2){b[0], b[1]}, acc, false);
-  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[2], a[3]}, (bf16x2){b[2], b[3]}, acc, false);
-  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[4], a[5]}, (bf16x2){b[4], b[5]}, acc, false);
-  acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[6], a[7]}, (bf16x2){b[6], b[7]}, acc, false);
-  return acc;
-}
 
 // LayerNorm of M <= MM <= 4 rows (K <= 4096) into LDS as bf16, 256 threads, nn.LayerNorm
 // semantics.  Each thread keeps its <= 16 values per row in registers: one global pass, ONE block

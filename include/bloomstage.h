@@ -167,6 +167,18 @@ int bs_head_slice(bs_stage *stage, const void *xn, int32_t batch, const uint64_t
  *   (:51-52); pass 1 to reproduce it.  Not available on vocabulary-slice (bs_head_slice) stages. */
 int bs_set_sampling(bs_stage *stage, int32_t top_k, float temperature, uint64_t seed);
 
+/* ---- Decode engine ----
+ * bf16 stages of hidden 1024 or 1536 (bloom-560m / bloom-1b1 widths) run a decode step of <= 2 rows
+ * (S = 1; contexts <= 1024 at one row, <= 512 at two) as ONE persistent launch of every decoder block
+ * (one workgroup per CU, the weights requested a layer ahead) instead of five launches per block.
+ * on = 1 uses it where it applies, 0 (the default) always takes the per-block launches.  Captured
+ * decode graphs are dropped.  Returns BS_OK. */
+int bs_set_decode_engine(bs_stage *stage, int32_t on);
+/* After a forward that used the engine: 1 if it did (the last call took it), and *status = its
+ * in-kernel timeout word (0 = every hand-off completed; nonzero = a wait expired after 200 ms and the
+ * step's results are invalid).  Synchronizes the stage's stream.  For tests and diagnostics. */
+int bs_engine_status(bs_stage *stage, int32_t *used, int32_t *status);
+
 /* Forget the cached positions of one KV row (slot), or of all rows when slot < 0. */
 int bs_reset_kv(bs_stage *stage, int32_t slot);
 /* Read back KV row `slot` of the stage's local layer `layer`, positions [pos0, pos0 + npos), as fp32

@@ -1,0 +1,165 @@
+"""GPU parity of the persistent decode engine (csrc/engine.hip) through the C-ABI.
+
+The engine runs every decoder block of a bf16 stage of hidden 1024 / 1536 for one decode step of <= 2
+rows in one launch (stage forward inference.cpp:145-218, one token per row).  Each test checks it three
+ways on the same seeded inputs:
+  * against the CPU checker (oracle/bloom_oracle.c, bf16 mode): logits at north_star's 2e-2 max-abs
+    (reduced depth), greedy ids equal unless the checker's top-2 margin is < 2e-2, hidden states of
+    middle stages within the wide-block bound, the K/V rows each step appends within one bf16 storage ulp;
+  * against the per-block launch path of the same library (bs_set_decode_engine(0)) on a twin stage;
+  * bs_engine_status: the step took the engine (used = 1) and no in-kernel wait expired (status = 0).
+Cases: bloom-1b1 width (h 1536, 16 heads, hd 96) and bloom-560m width (h 1024, 16 heads, hd 64);
+first+last, middle (hidden in and out) and first-only stages; one row, and two rows at different
+positions (bs_step.past_lens); contexts crossing 1..11 attention splits (64 positions each at one row,
+32 at two) up to the engine's one-row limit near 1024.
+"""
+import numpy as np
+import pytest
+
+from distributed_inference_demo_amd.stage import Stage
+from oracle import gen_np
+from oracle.oracle import OracleStage
+
+from test_gpu_parity import assert_ids_match, check_bf16_stored, check_close, check_logits
+
+pytestmark = pytest.mark.gpu
+
+
+def _kv_rows(o, layer, row, pos, nh, hd):
+    return np.stack([np.stack([o.read_kv(layer, w, row, hh, pos, hd) for hh in range(nh)])[:, None, :]
+                     for w in range(2)])
+
+
+def _trio(h, nh, L, V, lb, le, B, max_ctx, seed, is_first=None, is_last=None):
+    kw = dict(max_batch=B, max_ctx=max_ctx, seed=seed, is_first=is_first, is_last=is_last)
+    eng = Stage(h, nh, L, V, lb, le, dtype="bf16", max_tokens=B * 64, **kw)
+    eng.set_decode_engine(True)
+    lau = Stage(h, nh, L, V, lb, le, dtype="bf16", max_tokens=B * 64, **kw)
+    lau.set_decode_engine(False)
+    o = OracleStage(h, nh, L, V, lb, le, bf16=True, **kw)
+    return eng, lau, o
+
+
+@pytest.mark.parametrize("h", [1536, 1024])
+def test_engine_one_row_first_last_stage_through_many_splits(h):
+    """B = 1 decode from a 40-token prompt, teacher-forced with the checker's tokens, checked at
+    contexts 41..46, 100, 200, 330 (1..6 splits of 64 positions)."""
+    nh, L, V, P = 16, 3, 2048, 40
+    hd = h // nh
+    eng, lau, o = _trio(h, nh, L, V, 0, L, 1, 400, seed=71)
+    ids = gen_np.prompt_ids(73, 1, P, V).astype(np.int32)
+    te, lge = eng.forward_host(ids, 1, P, want_logits=True)
+    lau.forward_host(ids, 1, P)
+    to, lo = o.forward(ids, 1, P, want_logits=True)
+    check_logits(lge, lo, "bf16", f"h={h} prefill")
+    assert_ids_match(te, to, lo, f"h={h} prefill")
+    past, tok = P, to
+    checks = set(range(P, P + 6)) | {99, 199, 329}
+    while past < 330:
+        x = tok.reshape(1, 1)
+        if past in checks:
+            ge, le_ = eng.forward_host(x, 1, 1, past_len=past, want_logits=True)
+            assert eng.engine_status() == (1, 0)
+            gl, ll = lau.forward_host(x, 1, 1, past_len=past, want_logits=True)
+            assert lau.engine_status()[0] == 0
+            to, lo = o.forward(x, 1, 1, past_len=past, want_logits=True)
+            err = check_logits(le_, lo, "bf16", f"h={h} ctx {past + 1} engine vs checker")
+            check_logits(le_, ll, "bf16", f"h={h} ctx {past + 1} engine vs launches")
+            assert_ids_match(ge, to, lo, f"h={h} ctx {past + 1}")
+            for layer in range(L):
+                check_bf16_stored(eng.read_kv(layer, 0, past, 1), _kv_rows(o, layer, 0, past, nh, hd),
+                                  f"h={h} ctx {past + 1} new KV layer {layer}")
+            print(f"h={h} ctx {past + 1}: logits max-abs {err:.3e}")
+        else:
+            eng.forward_host(x, 1, 1, past_len=past)
+            lau.forward_host(x, 1, 1, past_len=past)
+            to = o.forward(x, 1, 1, past_len=past)
+        tok = to
+        past += 1
+    for s in (eng, lau, o):
+        s.close()
+
+
+@pytest.mark.parametrize("h", [1536, 1024])
+def test_engine_middle_stage_two_rows_at_different_positions(h):
+    """A middle stage (hidden in, hidden out; layers [2, 4) of a 6-layer model), two rows whose
+    contexts differ (prompts of 37 and 90 tokens): 12 decode steps with per-row positions, the
+    hidden states against the checker and the launch path."""
+    nh, Lm, V = 16, 6, 1024
+    eng, lau, o = _trio(h, nh, Lm, V, 2, 4, 2, 256, seed=81, is_first=False, is_last=False)
+    rng = np.random.default_rng(5)
+    lens = [37, 90]
+    for r, n in enumerate(lens):
+        x = rng.standard_normal((1, n, h)).astype(np.float32)
+        eng.forward_host(x, 1, n, slot=r, past_len=0)
+        lau.forward_host(x, 1, n, slot=r, past_len=0)
+        o.forward(x, 1, n, slot=r, past_len=0)
+    past = list(lens)
+    for step in range(12):
+        x = rng.standard_normal((2, 1, h)).astype(np.float32)
+        ye = eng.forward_host(x, 2, 1, past_len=past)
+        assert eng.engine_status() == (1, 0)
+        yl = lau.forward_host(x, 2, 1, past_len=past)
+        yo = np.concatenate([o.forward(x[r:r + 1], 1, 1, slot=r, past_len=past[r]) for r in range(2)])
+        check_close(ye, yo, "bf16", f"h={h} step {step} engine vs checker")
+        check_close(ye, yl, "bf16", f"h={h} step {step} engine vs launches")
+        past = [p + 1 for p in past]
+    for s in (eng, lau, o):
+        s.close()
+
+
+def test_engine_graph_replay_long_context_one_row():
+    """bloom-1b1 width, first + last stage, B = 1 on device buffers (graph replays, the bench's path):
+    free-running from a 16-token prompt to context 1000 (16 splits), checked against the checker at
+    contexts 257, 700 and 1000 after handing it the device's cache."""
+    import torch
+    h, nh, L, V, P = 1536, 16, 2, 2048, 16
+    hd = h // nh
+    g = Stage(h, nh, L, V, 0, L, dtype="bf16", max_batch=1, max_ctx=1024, max_tokens=P, seed=91)
+    g.set_decode_engine(True)
+    o = OracleStage(h, nh, L, V, 0, L, bf16=True, max_batch=1, max_ctx=1024, seed=91)
+    ids = gen_np.prompt_ids(93, 1, P, V).astype(np.int32)
+    dev = torch.device("cuda", 0)
+    cs = torch.cuda.Stream()
+    with torch.cuda.stream(cs):
+        tin = torch.from_numpy(ids).to(dev)
+        tok = torch.empty(1, dtype=torch.int32, device=dev)
+        lg = torch.empty((1, V), dtype=torch.float32, device=dev)
+        g.forward(tin, tok, 1, P, past_len=0, stream=cs.cuda_stream)
+        o.forward(ids, 1, P)
+        past = synced = P
+        for ctx in (257, 700, 1000):
+            while past < ctx - 1:
+                g.forward(tok, tok, 1, 1, past_len=past, stream=cs.cuda_stream)
+                past += 1
+            cs.synchronize()
+            for layer in range(L):
+                o.write_kv(layer, 0, synced, g.read_kv(layer, 0, synced, past - synced))
+            t_in = tok.cpu().numpy()
+            g.forward(tok, tok, 1, 1, past_len=past, logits=lg, stream=cs.cuda_stream)
+            to, lo = o.forward(t_in.reshape(1, 1), 1, 1, past_len=past, want_logits=True)
+            cs.synchronize()
+            assert g.engine_status() == (1, 0)
+            err = check_logits(lg.cpu().numpy(), lo, "bf16", f"ctx {ctx}")
+            assert_ids_match(tok.cpu().numpy(), to, lo, f"ctx {ctx}")
+            for layer in range(L):
+                check_bf16_stored(g.read_kv(layer, 0, past, 1), _kv_rows(o, layer, 0, past, nh, hd),
+                                  f"ctx {ctx} new KV layer {layer}")
+            print(f"graph ctx {ctx}: logits max-abs {err:.3e}")
+            past += 1
+            synced = past
+    g.close()
+    o.close()
+
+
+def test_engine_not_taken_outside_its_shapes():
+    """Three rows, int8 weights, fp32 and a hidden width of 2560 keep the per-block launches."""
+    for kw in (dict(h=1536, B=3, dtype="bf16"), dict(h=2560, B=1, dtype="bf16"), dict(h=1024, B=1, dtype="fp32")):
+        h, B = kw["h"], kw["B"]
+        g = Stage(h, h // 64 if h == 2560 else 16, 1, 512, 0, 1, dtype=kw["dtype"], max_batch=B, max_ctx=32, seed=3)
+        g.set_decode_engine(True)
+        ids = gen_np.prompt_ids(5, B, 4, 512).astype(np.int32)
+        g.forward_host(ids, B, 4)
+        g.forward_host(ids[:, :1], B, 1, past_len=4)
+        assert g.engine_status()[0] == 0, kw
+        g.close()
