@@ -88,6 +88,15 @@ struct AttnArgs {
   int chunk;           // positions per chunk (decode) = 64
   unsigned* tickets;   // [max_batch][n_head] split-merge tickets (zero between launches)
   int defer_merge;     // decode split > 1: leave the partials for the consumer (launch_linear_parts)
+  // prefill (S > 1) split-KV: key tiles of a 64-query tile spread over blocks of `pf_tiles` 64-key
+  // tiles each (0: no split); partials [item][split][64 queries][4 + head_dim] in pf_ws (pf_cap floats), one
+  // ticket per (row, head, query tile) in pf_tickets (zero between launches, pf_ntickets of them)
+  int pf_tiles;
+  float* pf_ws;
+  size_t pf_cap;
+  unsigned* pf_tickets;
+  int pf_ntickets;
+  int pf_past_max;     // largest past_len of the call's rows (sizes the split grid)
 };
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s);
 size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, int* max_chunks, int* chunk);

@@ -1345,10 +1345,13 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(const bf16* __restrict__
 // bias and int8 column scale per output column j, the residual per element, the cached positions per
 // output row.  Loaded unconditionally at clamped indices: an exec-masked or per-element load in the
 // epilogue makes hipcc wait for each one in turn (16-64 dependent round trips per thread).
+// The residual is prefetched only for small tiles (TM * TN <= 4): a 128x128 tile's 64 values per lane would
+// stay live across the whole K loop; its epilogue reads them where it uses them.
+template <int TM, int TN> struct ResidPre { static constexpr bool on = TM * TN <= 4; };
 template <int TM, int TN, int EK>
 struct GemmEpiPre {
   float bias[TN], cscale[TN];
-  float resid[EK == EPI_RESID ? TM * TN * 4 : 1];
+  float resid[EK == EPI_RESID && ResidPre<TM, TN>::on ? TM * TN * 4 : 1];
   int past[EK == EPI_QKV ? TM * 4 : 1];
 };
 
@@ -1363,7 +1366,7 @@ __device__ __forceinline__ void gemm_epi_prefetch(GemmEpiPre<TM, TN, EK>& pre, c
       pre.bias[j] = to_f32(((const bf16*)ep.bias)[n]);
       pre.cscale[j] = ep.col_scale ? ep.col_scale[n] : 1.f;
     }
-    if constexpr (EK == EPI_RESID) {
+    if constexpr (EK == EPI_RESID && ResidPre<TM, TN>::on) {
 #pragma unroll
       for (int i = 0; i < TM; i++)
 #pragma unroll
@@ -1419,7 +1422,8 @@ __device__ __forceinline__ void gemm_epi_store(const f32x4 (&acc)[TM][TN], const
               ((bf16*)(which == 1 ? ep.k_cache : ep.v_cache))[idx] = from_f32<bf16>(v);
             }
           } else if constexpr (EK == EPI_RESID) {
-            ep.out_f32[(size_t)m * ep.ldo + n] = v + pre.resid[(i * 4 + e) * TN + j];
+            const float rs = ResidPre<TM, TN>::on ? pre.resid[(i * 4 + e) * TN + j] : ep.resid[(size_t)m * ep.ldo + n];
+            ep.out_f32[(size_t)m * ep.ldo + n] = v + rs;
           } else {
             ((bf16*)ep.out_act)[(size_t)m * ep.ldo + n] = from_f32<bf16>(gelu_bloom(v));
           }
@@ -1428,6 +1432,12 @@ __device__ __forceinline__ void gemm_epi_store(const f32x4 (&acc)[TM][TN], const
   }
 }
 
+// Split-K (gridDim.z = KS > 1, K % (KS * 64) == 0): block z computes columns [z K / KS, (z + 1) K / KS) of
+// the dot products, stores its partial tile write-through (sc1) to ep.sk_ws in fragment order
+// ([tile][z][wave][i][j][lane] f32x4: 16 B per lane, coalesced) and takes the tile's ticket; the block
+// drawing the last ticket sums the KS partials in z order (its own from registers: the same order
+// whichever block arrives last, so results do not depend on timing), resets the ticket and runs the
+// epilogue.  MI355X_MICROARCH.md "Valid forms" row 1 (counter form, the last adder reads).
 template <int BM, int BN, int PS, int EK>
 __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                                          int M, int N, int K, Epi ep) {
@@ -1439,6 +1449,7 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1, r = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int KS = gridDim.z, kz = blockIdx.z, Kz = K / KS;  // this block's K range: [kz Kz, (kz + 1) Kz)
   auto sw = [](int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); };  // element offset
   auto row_m = [&](int i, int e) { return m0 + wm * (BM / 2) + i * 16 + 4 * g + e; };
   auto col_n = [&](int j) { return n0 + wn * (BN / 2) + j * 16 + r; };
@@ -1451,16 +1462,16 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
 #pragma unroll
   for (int i = 0; i < CA; i++) {
     const int c = tid + i * 256, row = c >> 3, ch = c & 7;
-    ga[i] = X + (size_t)min(m0 + row, M - 1) * K + ch * 8;
+    ga[i] = X + (size_t)min(m0 + row, M - 1) * K + (size_t)kz * Kz + ch * 8;
     la[i] = sw(row, ch);
   }
 #pragma unroll
   for (int i = 0; i < CB; i++) {
     const int c = tid + i * 256, row = c >> 3, ch = c & 7;
-    gb[i] = W + (size_t)min(n0 + row, N - 1) * K + ch * 8;
+    gb[i] = W + (size_t)min(n0 + row, N - 1) * K + (size_t)kz * Kz + ch * 8;
     lb[i] = sw(row, ch);
   }
-  const int nk = K / BK;
+  const int nk = Kz / BK;
   bf16x8 ra[PS][CA], rb[PS][CB];
   auto gload = [&](int st, int kt) {  // tile kt -> register stage st (clamped: a re-read past the end is unused)
     const size_t off = (size_t)min(kt, nk - 1) * BK;
@@ -1529,13 +1540,276 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
       cur ^= 1;
     }
   }
+  if (KS > 1) {
+    __shared__ int last;
+    const size_t tile = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    float* base = ep.sk_ws + tile * KS * (BM * BN);
+    const __amdgpu_buffer_rsrc_t rs = attn_rsrc(base);
+    auto off = [&](int z, int i, int j) { return (uint32_t)(((((z * 4 + w) * TM + i) * TN + j) * 64 + lane) * 16); };
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+      for (int j = 0; j < TN; j++)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc[i][j]), rs, off(kz, i, j), 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      typedef __attribute__((address_space(1))) unsigned gu32;
+      const unsigned old = __hip_atomic_fetch_add((gu32*)(ep.sk_tickets + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = old == (unsigned)(KS - 1);
+      if (last) __hip_atomic_store((gu32*)(ep.sk_tickets + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+      for (int j = 0; j < TN; j++) {
+        f32x4 t = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int z = 0; z < KS; z++)
+          t += z == kz ? acc[i][j] : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off(z, i, j), 0, 16));
+        acc[i][j] = t;
+      }
+  }
   gemm_epi_store(acc, pre, ep, M, N, row_m, col_n);
+}
+
+// ------------------------------------------------------------------------------------
+// gemm_mfma3: prefill GEMM on v_mfma_f32_32x32x16_bf16 (measured 2184 TFLOP/s against 1272 for the 16x16x32
+// form, bs_mfma_probe).  128 x 128 tile, 256 threads as 2 x 2 waves of 64 x 64 (2 x 2 accumulators of
+// 32 x 32), BK = 64, LDS double buffer (one __shared__ array) fed from a 2-deep register ring.  A wave
+// reads 16 KB of fragments per 64 K-columns for 262 K MACs: half the LDS bytes per MAC of the 64 x 64
+// tile's 32 x 32 waves, and a quarter of the MFMA instructions.  At prefill sizes the tile count is small (bloom-1b1 QKV at 512 tokens:
+// 144 tiles), so K is split over gridDim.z = KS blocks (fragment-order fp32 slabs, write-through, the
+// last-arriving block of a tile sums them in z order: deterministic whichever block arrives last).
+// Fragment maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) holds A[row r][k 8h + j]
+// = X[m][k] and B[k 8h + j][col r] = W[n][k]; accumulator register e is row (e & 3) + 8 (e >> 2) + 4 h,
+// column r.  LDS rows are 128 B with the 16-B chunk index XOR-swizzled by (row >> 1) & 7: the 16 lanes
+// of a ds_read_b128 pass (rows 2k, 2k + 1 in the two halves of a 256-B bank row) hit 16 distinct slots.
+// ------------------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int EK, int PS>
+__global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
+                                                         int M, int N, int K, Epi ep) {
+  constexpr int BM = 128, BN = 128, BK = 64;
+  constexpr int CA = BM * BK / 8 / 256, CB = BN * BK / 8 / 256;  // 16-B chunks per thread per stage: 4, 4
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * BK];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1, r = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int KS = gridDim.z, kz = blockIdx.z, Kz = K / KS;
+  auto sw = [](int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); };
+  auto As = [&](int buf) { return smem + buf * (BM + BN) * BK; };
+  auto Bs = [&](int buf) { return smem + buf * (BM + BN) * BK + BM * BK; };
+
+  // buffer loads: a 32-bit byte offset per lane and the K position as the scalar offset (the host checks
+  // M * K and N * K bf16 fit 4 GB)
+  const __amdgpu_buffer_rsrc_t rx = attn_rsrc(X), rw = attn_rsrc(W);
+  uint32_t oa[CA], ob[CB];
+  int la[CA];
+#pragma unroll
+  for (int i = 0; i < CA; i++) {
+    const int c = tid + i * 256, row = c >> 3, ch = c & 7;
+    oa[i] = (uint32_t)(((size_t)min(m0 + row, M - 1) * K + (size_t)kz * Kz + ch * 8) * 2);
+    ob[i] = (uint32_t)(((size_t)min(n0 + row, N - 1) * K + (size_t)kz * Kz + ch * 8) * 2);
+    la[i] = sw(row, ch);
+  }
+  float bias[2], cscale[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const int n = min(n0 + wn * 64 + j * 32 + r, N - 1);
+    bias[j] = EK == EPI_ARGMAX ? 0.f : to_f32(((const bf16*)ep.bias)[n]);
+    cscale[j] = ep.col_scale ? ep.col_scale[n] : 1.f;
+  }
+  const int nk = Kz / BK;
+  bf16x8 ra[PS][CA], rb[PS][CB];
+  auto gload = [&](int st, int kt) {  // tile kt -> register stage st (clamped: a re-read past the end is unused)
+#ifdef GEMM3_ABLATE_LOADS
+    if (kt >= PS) return;
+#endif
+    const int off = min(kt, nk - 1) * BK * 2;
+#pragma unroll
+    for (int i = 0; i < CA; i++) ra[st][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, oa[i], off, 0));
+#pragma unroll
+    for (int i = 0; i < CB; i++) rb[st][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ob[i], off, 0));
+  };
+  auto lstore = [&](int st, int buf) {
+#pragma unroll
+    for (int i = 0; i < CA; i++) *reinterpret_cast<bf16x8*>(As(buf) + la[i]) = ra[st][i];
+#pragma unroll
+    for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(Bs(buf) + la[i]) = rb[st][i];
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+      for (int e = 0; e < 16; e++) acc[i][j][e] = 0.f;
+  auto ktile = [&](int buf) {
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ks++) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; i++) af[i] = *reinterpret_cast<const bf16x8*>(As(buf) + sw(wm * 64 + i * 32 + r, ks * 2 + h));
+#pragma unroll
+      for (int j = 0; j < 2; j++) bfr[j] = *reinterpret_cast<const bf16x8*>(Bs(buf) + sw(wn * 64 + j * 32 + r, ks * 2 + h));
+#ifdef GEMM3_ABLATE_MFMA
+      acc[0][0][0] += (float)af[0][0] + (float)af[1][1] + (float)bfr[0][2] + (float)bfr[1][3];
+#else
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+#endif
+    }
+  };
+  // the ring of gemm_mfma2 (PS = 2): full groups run with no conditions, so the loads are counted with vmcnt(N)
+#pragma unroll
+  for (int st = 0; st < PS; st++) gload(st, st);
+  lstore(0, 0);
+  gload(0, PS);
+  __syncthreads();
+  int cur = 0, kt0 = 0;
+  for (; kt0 + PS <= nk; kt0 += PS) {
+#pragma unroll
+    for (int s2 = 0; s2 < PS; s2++) {
+      const int kt = kt0 + s2, nst = (s2 + 1) % PS;
+      ktile(cur);
+      lstore(nst, cur ^ 1);
+      gload(nst, kt + 1 + PS);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < PS; s2++) {  // tail: nk % PS steps
+    const int kt = kt0 + s2, nst = (s2 + 1) % PS;
+    if (kt < nk) {
+      ktile(cur);
+      lstore(nst, cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  if (KS > 1) {
+    const size_t tile = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const __amdgpu_buffer_rsrc_t rs = attn_rsrc(ep.sk_ws + tile * KS * (BM * BN));
+    auto off = [&](int z, int i, int j, int q) { return (uint32_t)((((((z * 4 + w) * 2 + i) * 2 + j) * 4 + q) * 64 + lane) * 16); };
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs, off(kz, i, j, q), 0, 16);
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);  // the LDS tiles are dead: the flag rides in the one array
+    if (tid == 0) {
+      typedef __attribute__((address_space(1))) unsigned gu32;
+      const unsigned old = __hip_atomic_fetch_add((gu32*)(ep.sk_tickets + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == (unsigned)(KS - 1);
+      if (last) __hip_atomic_store((gu32*)(ep.sk_tickets + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    // every slab (this block's too) re-read unconditionally and summed in z order
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        f32x4 t[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+        for (int z = 0; z < KS; z++) {
+          f32x4 v[4];
+#pragma unroll
+          for (int q = 0; q < 4; q++) v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off(z, i, j, q), 0, 16));
+#pragma unroll
+          for (int q = 0; q < 4; q++) t[q] += v[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+          for (int e = 0; e < 4; e++) acc[i][j][4 * q + e] = t[q][e];
+      }
+  }
+  // epilogue: per accumulator, its 16 per-element / per-row operands are loaded in one batch (clamped,
+  // unconditional: a guarded load per element would wait for each in turn), then the stores
+  auto row_of = [&](int i, int e) { return m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h; };
+  auto col_of = [&](int j) { return n0 + wn * 64 + j * 32 + r; };
+  if constexpr (EK == EPI_RESID) {
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        float rsd[16];
+#pragma unroll
+        for (int e = 0; e < 16; e++) rsd[e] = ep.resid[(size_t)min(row_of(i, e), M - 1) * ep.ldo + min(col_of(j), N - 1)];
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+          const int m = row_of(i, e), n = col_of(j);
+          if (m < M && n < N) ep.out_f32[(size_t)m * ep.ldo + n] = acc[i][j][e] * cscale[j] + bias[j] + rsd[e];
+        }
+      }
+  } else if constexpr (EK == EPI_GELU) {
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+          const int m = row_of(i, e), n = col_of(j);
+          if (m < M && n < N)
+            ((bf16*)ep.out_act)[(size_t)m * ep.ldo + n] = from_f32<bf16>(gelu_bloom(acc[i][j][e] * cscale[j] + bias[j]));
+        }
+  } else if constexpr (EK == EPI_QKV) {
+    const int three = 3 * ep.head_dim;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      int past[16];
+#pragma unroll
+      for (int e = 0; e < 16; e++) past[e] = ep.past_dev ? ep.past_dev[min(row_of(i, e), M - 1) / ep.seq] : ep.past;
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const int n = col_of(j);
+        const int head = n / three, rr = n - head * three, which = rr / ep.head_dim, d = rr - which * ep.head_dim;
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+          const int m = row_of(i, e);
+          if (m >= M || n >= N) continue;
+          const bf16 v = from_f32<bf16>(acc[i][j][e] * cscale[j] + bias[j]);
+          if (which == 0) {
+            ((bf16*)ep.q_out)[(size_t)m * ep.hidden + head * ep.head_dim + d] = v;
+          } else {
+            const int b = m / ep.seq, t = m - b * ep.seq;
+            const size_t idx = (((size_t)(ep.slot + b) * ep.n_head + head) * ep.max_ctx + past[e] + t) * ep.head_dim + d;
+            ((bf16*)(which == 1 ? ep.k_cache : ep.v_cache))[idx] = v;
+          }
+        }
+      }
+    }
+  }
+}
+
+// gemm_mfma3_kernel launch: K % (KS * 64) == 0; KS > 1 needs ep.sk_ws / sk_tickets room (gemm3_split_k).
+template <int PS = 2>
+static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int KS) {
+  dim3 grid((N + 127) / 128, (M + 127) / 128, KS);
+  switch (ep.kind) {
+    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, PS><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, PS><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
+    default: gemm_mfma3_kernel<EPI_GELU, PS><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
+  }
 }
 
 // gemm_mfma2_kernel with the epilogue kind as a template argument.
 template <int BM, int BN, int PS>
-static void gemm2_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s) {
-  const dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
+static void gemm2_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int KS = 1) {
+  const dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, KS);
   switch (ep.kind) {
     case EPI_QKV: gemm_mfma2_kernel<BM, BN, PS, EPI_QKV><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
     case EPI_RESID: gemm_mfma2_kernel<BM, BN, PS, EPI_RESID><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
@@ -1743,6 +2017,23 @@ void launch_linear_parts(const AttnParts& p, const void* W, int M, int N, int K,
   gemv_rows_dispatch<X_PARTS>(nullptr, LnArgs{}, p, (const bf16*)W, M, N, K, ep, s);
 }
 
+// Split-K factor of a 64x64-tile prefill GEMM: only the long-K shapes (fc2: K = 4h) gain from it -- KS
+// about 768 / tiles (2..4 work items per CU), K / KS >= 1024 columns per split, the partials fitting the
+// workspace; every other shape runs whole-K tiles (tools/gemm_splitk_bench.hip, profiles/r03_gemm_splitk.txt:
+// bloom-1b1 fc2 at 512 tokens 31.8 -> 28.6 us with KS = 4, bloom-7b1 fc2 126.3 -> 122.8 with KS = 2; QKV,
+// dense and fc1 only lose).
+static int gemm_split_k(int M, int N, int K, const Epi& ep) {
+  if (!ep.sk_ws || !ep.sk_tickets || K < 4096) return 1;
+  const long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
+  if (tiles > ep.sk_ntickets) return 1;
+  for (int ks = 4; ks >= 2; ks--) {
+    if (K % (ks * 64) || K / ks < 1024 || tiles * ks > 1024) continue;
+    if ((size_t)tiles * ks * 64 * 64 > ep.sk_cap) continue;
+    return ks;
+  }
+  return 1;
+}
+
 void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int K, const Epi& ep, hipStream_t s) {
   if (M <= 0) return;
   if (!is_bf16) {
@@ -1761,13 +2052,13 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
     if (blocks(128, 128) >= 240) {
       gemm2_launch<128, 128, 1>(x, w, M, N, K, ep, s);
-    } else if (blocks(64, 64) >= 240) {
-      // below 240 128x128 tiles the K loop is latency-bound: 64x64 tiles with a 4-deep ring beat
-      // 128x64 (profiles/r01_gemm_tile_sweep.txt: bloom-1b1 S=512 prefill 4.56 -> 4.42 ms)
-      gemm2_launch<64, 64, 4>(x, w, M, N, K, ep, s);
+    } else if (blocks(64, 64) >= 128) {
+      // below 240 128x128 tiles the K loop is latency-bound: 64x64 tiles with a 4-deep ring (beat 128x64,
+      // profiles/r01_gemm_tile_sweep.txt, and 64x32 even at 192 tiles: bloom-1b1 dense 13.0 -> 12.4 us,
+      // profiles/r03_gemm_splitk.txt), split-K for the long-K fc2 shapes
+      gemm2_launch<64, 64, 4>(x, w, M, N, K, ep, s, gemm_split_k(M, N, K, ep));
     } else {
-      // narrow N at prefill sizes (bloom-1b1 dense / fc2 at 512 tokens: 192 64x64 tiles): 64x32
-      // tiles put >= 1 block on every CU, and a second block on many, to hide the K loop's loads
+      // fewer than 128 64x64 tiles (a few hundred tokens of a narrow GEMM): 64x32 tiles for more blocks
       gemm2_launch<64, 32, 4>(x, w, M, N, K, ep, s);
     }
     return;
@@ -2057,7 +2348,10 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) _Float16 Ps[4][16 * VLD];
   __shared__ __attribute__((aligned(16))) _Float16 Pl[4][16 * VLD];  // p - fp16(p): P keeps ~21 bits
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
-  const int qt = gridDim.x - 1 - blockIdx.x, head = blockIdx.y, b = blockIdx.z;
+  // split-KV (a.pf_tiles > 0): blockIdx.x = (query tile, key split); heaviest query tiles first
+  const int nspl = gridDim.x / ((a.S + 63) / 64);
+  const int qt = (gridDim.x - 1 - blockIdx.x) / nspl, spl = (gridDim.x - 1 - blockIdx.x) % nspl;
+  const int head = blockIdx.y, b = blockIdx.z;
   const int hd = a.head_dim;
   const int past = a.past_dev ? a.past_dev[b] : a.past;
   const int q0 = qt * 64 + w * 16;          // first query (within this call) of the wave
@@ -2083,8 +2377,10 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   for (int i = 0; i < 4; i++) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
 #pragma unroll
   for (int t = 0; t < NT; t++) o[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  // keys visible to the block's last query
+  // keys visible to the block's last query; a split takes key tiles [spl * pf_tiles, + pf_tiles)
   const int kend = past + min(a.S, qt * 64 + 64);
+  const int kbeg = nspl > 1 ? min(spl * a.pf_tiles * KT, kend) : 0;
+  const int kstop = nspl > 1 ? min(kbeg + a.pf_tiles * KT, kend) : kend;
   const int nchunk = hd / 8, nch = KT * nchunk;
   // the padded dims are never staged: zero them once (keeps the MFMA inputs finite)
   if (HDP != 0) {
@@ -2101,8 +2397,10 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   // (a thread per item; KT/4 * hd/8 <= 256 items)
   const int nvi = (KT / 4) * nchunk;
   const int vq = min(tid, nvi - 1) / nchunk, vdc = (min(tid, nvi - 1) % nchunk) * 8;
+  // one register stage: tile k0 + KT is in flight while tile k0 computes (a second stage, tile k0 + 2 KT,
+  // measured no faster: profiles/r03_attn_prefill_split.txt)
   bf16x8 kreg[CPT], vreg[4];
-  auto gload = [&](int k0) {
+  auto gload = [&](int k0) {  // clamped: loads past the block's keys re-read its last key
 #pragma unroll
     for (int i = 0; i < CPT; i++) {
       const int c = min(tid + i * 256, nch - 1);
@@ -2116,8 +2414,8 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       vreg[i] = *reinterpret_cast<const bf16x8*>(vb + (size_t)key * hd + vdc);
     }
   };
-  gload(0);
-  for (int k0 = 0; k0 < kend; k0 += KT) {
+  if (kbeg < kstop) gload(kbeg);
+  for (int k0 = kbeg; k0 < kstop; k0 += KT) {
     __syncthreads();  // previous tile's LDS reads are done
 #pragma unroll
     for (int i = 0; i < CPT; i++) {
@@ -2137,7 +2435,7 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       }
     }
     __syncthreads();
-    if (k0 + KT < kend) gload(k0 + KT);  // next tile in flight while this one computes
+    if (k0 + KT < kstop) gload(k0 + KT);  // next tile in flight while this one computes
     // S tiles: four 16-key tiles
     f32x4 sacc[4];
 #pragma unroll
@@ -2158,7 +2456,7 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         const int kpos = k0 + t * 16 + r;
-        const float v = (kpos <= qpos && kpos < kend) ? slope * (float)kpos + a.inv_norm * sacc[t][i] : -INFINITY;
+        const float v = (kpos <= qpos && kpos < kstop) ? slope * (float)kpos + a.inv_norm * sacc[t][i] : -INFINITY;
         sv[t][i] = v;
         rmax[i] = fmaxf(rmax[i], v);
       }
@@ -2218,6 +2516,92 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       }
     }
   }
+  if (nspl > 1) {
+    // split partial (running max, sum, unnormalised context) of the block's 64 queries, write-through:
+    // record [m, l, -, -, o[0..hd)] per (split, query); the block drawing the last ticket of its (row,
+    // head, query tile) merges the splits in split order
+    const int rs = hd + 4;
+    const size_t item = ((size_t)(b * a.n_head + head) * ((a.S + 63) / 64) + qt);
+    const __amdgpu_buffer_rsrc_t rp = attn_rsrc(a.pf_ws + item * nspl * 64 * rs);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int ql = w * 16 + 4 * g + i;
+      const uint32_t rec = (uint32_t)((spl * 64 + ql) * rs) * 4;
+      if (r == 0) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m_run[i]), rp, rec, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l_run[i]), rp, rec + 4, 0, 16);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        const int d = t * 16 + r;
+        if (d < hd) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o[t][i]), rp, rec + (4 + d) * 4, 0, 16);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int last;
+    __syncthreads();
+    if (tid == 0) {
+      typedef __attribute__((address_space(1))) unsigned gu32;
+      const unsigned old = __hip_atomic_fetch_add((gu32*)(a.pf_tickets + item), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = old == (unsigned)(nspl - 1);
+      if (last) __hip_atomic_store((gu32*)(a.pf_tickets + item), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    // merge: 4 threads per query, each a quarter of its 4-dim chunks; splits in groups of 4 whose loads
+    // are all issued before use (indices clamped, surplus splits weighted 0), online max across groups
+    const int ql = tid >> 2, j = tid & 3, nc = hd / 4;
+    constexpr int G = 4, NC = HDP / 16;  // chunks per thread: ceil(HDP/4 / 4)
+    float M = -INFINITY, Lsum = 0.f;
+    f32x4 acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) acc[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < nspl; s0 += G) {
+      float mg[G], lg[G];
+      f32x4 og[G][NC];
+#pragma unroll
+      for (int u = 0; u < G; u++) {
+        const uint32_t rec = (uint32_t)((min(s0 + u, nspl - 1) * 64 + ql) * rs) * 4;
+        mg[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, rec, 0, 16));
+        lg[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, rec + 4, 0, 16));
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+          og[u][c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rp, rec + (4 + 4 * min(j + 4 * c, nc - 1)) * 4, 0, 16));
+      }
+      float mn = M;
+#pragma unroll
+      for (int u = 0; u < G; u++)
+        if (s0 + u < nspl) mn = fmaxf(mn, mg[u]);
+      const float sc = M == -INFINITY ? 0.f : __expf(M - mn);  // mn is finite: split 0 holds key 0
+      Lsum *= sc;
+#pragma unroll
+      for (int c = 0; c < NC; c++) acc[c] *= sc;
+#pragma unroll
+      for (int u = 0; u < G; u++) {
+        // a split past the query's keys (m = -inf) or past nspl weighs 0
+        const float wu = (s0 + u < nspl && mg[u] != -INFINITY) ? __expf(mg[u] - mn) : 0.f;
+        Lsum += wu * lg[u];
+#pragma unroll
+        for (int c = 0; c < NC; c++) acc[c] += wu * og[u][c];
+      }
+      M = mn;
+    }
+    const int q = qt * 64 + ql;
+    if (q < a.S) {
+      const float inv = 1.f / Lsum;
+      bf16* op = (bf16*)a.ctx_out + ((size_t)b * a.S + q) * a.hidden + head * hd;
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        const int ch = j + 4 * c;
+        if (ch < nc) {
+          bf16 v4[4] = {(bf16)(acc[c][0] * inv), (bf16)(acc[c][1] * inv), (bf16)(acc[c][2] * inv), (bf16)(acc[c][3] * inv)};
+          *reinterpret_cast<uint2*>(op + 4 * ch) = *reinterpret_cast<const uint2*>(v4);
+        }
+      }
+    }
+    return;
+  }
   // write ctx rows (q = q0 + 4g + i, dim = t*16 + r)
 #pragma unroll
   for (int i = 0; i < 4; i++) {
@@ -2274,7 +2658,17 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
     }
   } else {
     if (is_bf16 && a.head_dim <= 128) {
-      dim3 g((a.S + 63) / 64, a.n_head, a.B);
+      // split-KV: a query tile's keys over ceil(tiles / pf_tiles) blocks when the grid would leave CUs idle
+      // and the partials fit (the longest query tile otherwise walks every key tile alone)
+      const int nqt = (a.S + 63) / 64;
+      const int ktiles = (a.pf_past_max + a.S + 63) / 64;  // the last query tile's, longest row
+      int nspl = 1;
+      if (a.pf_tiles > 0 && a.pf_ws && a.pf_tickets && (long)nqt * a.n_head * a.B < 256 && ktiles > a.pf_tiles) {
+        nspl = (ktiles + a.pf_tiles - 1) / a.pf_tiles;
+        const size_t need = (size_t)a.B * a.n_head * nqt * nspl * 64 * (a.head_dim + 4);
+        if (need > a.pf_cap || (long)a.B * a.n_head * nqt > a.pf_ntickets) nspl = 1;
+      }
+      dim3 g(nqt * nspl, a.n_head, a.B);
       const int hdp = (a.head_dim + 31) / 32 * 32;
       if (hdp <= 64) attn_prefill_mfma_kernel<64><<<g, 256, 0, s>>>(a);
       else if (hdp <= 96) attn_prefill_mfma_kernel<96><<<g, 256, 0, s>>>(a);

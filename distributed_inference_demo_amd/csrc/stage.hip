@@ -72,7 +72,8 @@ struct ProfClass {
 // Split-K workspace of the batched decode GEMV (kernels.hip gemv_tiles_dispatch): up to 16 splits
 // of 32 rows x 4096 columns, one ticket per 16-column tile.  Used only by enqueue_forward's GEMVs
 // (one stream per stage); head slices on another stream never split K.
-constexpr size_t kSkCap = (size_t)16 * 32 * 4096;
+// Also the prefill GEMM's split-K partials (kernels.hip gemm_split_k: at most ~480 128x128 tiles' worth).
+constexpr size_t kSkCap = (size_t)480 * 128 * 128;
 constexpr int kSkTickets = 4096;
 
 struct bs_stage {
@@ -1114,6 +1115,10 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     a.B = B; a.S = S; a.slot = slot; a.past = past; a.past_dev = past_dev; a.n_head = nh; a.head_dim = hd;
     a.max_ctx = d.max_ctx; a.hidden = h; a.inv_norm = inv_norm; a.part_acc = s->part_acc; a.part_ml = s->part_ml;
     a.max_chunks = s->max_chunks; a.chunk = s->chunk; a.tickets = s->att_tickets;
+    // prefill: the long query tiles' keys split over blocks of 4 key tiles, partials in the GEMM split-K
+    // workspace (free between the QKV GEMM and the dense GEMM on this stream)
+    a.pf_tiles = 4; a.pf_ws = s->sk_ws; a.pf_cap = kSkCap; a.pf_tickets = s->sk_tickets; a.pf_ntickets = kSkTickets;
+    a.pf_past_max = *std::max_element(pasts.begin(), pasts.end());
     // a split decode context merges in the dense GEMV's prologue when that kernel can take it
     const int nsplit = S == 1 ? attention_decode_splits(B, nh, s->max_chunks) : 1;
     a.defer_merge = s->bf16 && nsplit > 1 &&

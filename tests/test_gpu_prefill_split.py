@@ -1,0 +1,64 @@
+"""GPU parity of the split-KV prefill attention (kernels.hip attn_prefill_mfma_kernel).
+
+When a prefill's (rows x heads x 64-query tiles) grid is under 256 blocks, each query tile's keys are
+split over blocks of four 64-key tiles whose partial (max, sum, context) records the last-arriving block
+merges in split order.  These cases run through that path and check the stage's hidden states against
+the CPU checker (oracle/bloom_oracle.c, bf16 mode) at the wide-block bound, per row and per query tile:
+  * head dims 64 / 96 / 128 (hidden 1024 / 1536 / 2048, 16 heads);
+  * one row, 512 tokens from an empty cache (8 query tiles, 1..8 key tiles, 2 splits);
+  * two rows continuing from different cached lengths (130 and 450 positions, per-row bs_step.past_lens):
+    row 1's last query tile sees 11 key tiles (3 splits), row 0's at most 6, so its third split is empty;
+  * short prompts (130 tokens: 3 key tiles, one block per query tile) that seed the continuation.
+"""
+import numpy as np
+import pytest
+
+from distributed_inference_demo_amd.stage import Stage
+from oracle.oracle import OracleStage
+
+from test_gpu_parity import check_close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("h", [1024, 1536, 2048])
+def test_prefill_split_kv_one_row_512(h):
+    nh, S = 16, 512
+    gs = Stage(h, nh, 1, 512, 0, 1, dtype="bf16", max_batch=1, max_ctx=S, max_tokens=S, seed=101,
+               is_first=False, is_last=False)
+    os_ = OracleStage(h, nh, 1, 512, 0, 1, bf16=True, max_batch=1, max_ctx=S, seed=101, is_first=False,
+                      is_last=False)
+    x = np.random.default_rng(7).standard_normal((1, S, h)).astype(np.float32)
+    yg = gs.forward_host(x, 1, S, past_len=0)
+    yo = os_.forward(x, 1, S, past_len=0)
+    err = check_close(yg, yo, "bf16", f"h={h} prefill 1x{S}")
+    for t in range(0, S, 64):
+        check_close(yg[:, t:t + 64], yo[:, t:t + 64], "bf16", f"h={h} query tile {t // 64}")
+    print(f"h={h}: prefill 1x{S} max-abs {err:.3e}")
+    gs.close()
+    os_.close()
+
+
+@pytest.mark.parametrize("h", [1024, 1536])
+def test_prefill_split_kv_two_rows_continuing_from_different_lengths(h):
+    nh, S2, L = 16, 200, 2
+    lens = [130, 450]
+    kw = dict(max_batch=2, max_ctx=1024, seed=103, is_first=False, is_last=False)
+    gs = Stage(h, nh, L, 512, 0, L, dtype="bf16", max_tokens=2 * 512, **kw)
+    os_ = OracleStage(h, nh, L, 512, 0, L, bf16=True, **kw)
+    rng = np.random.default_rng(11)
+    for r, n in enumerate(lens):
+        x = rng.standard_normal((1, n, h)).astype(np.float32)
+        yg = gs.forward_host(x, 1, n, slot=r, past_len=0)
+        yo = os_.forward(x, 1, n, slot=r, past_len=0)
+        check_close(yg, yo, "bf16", f"h={h} row {r} prompt {n}")
+    x = rng.standard_normal((2, S2, h)).astype(np.float32)
+    yg = gs.forward_host(x, 2, S2, past_len=lens)
+    for r in range(2):
+        yo = os_.forward(x[r:r + 1], 1, S2, slot=r, past_len=lens[r])
+        err = check_close(yg[r:r + 1], yo, "bf16", f"h={h} row {r} continuation from {lens[r]}")
+        for t in range(0, S2, 64):
+            check_close(yg[r:r + 1, t:t + 64], yo[:, t:t + 64], "bf16", f"h={h} row {r} query tile {t // 64}")
+        print(f"h={h} row {r}: continuation {S2} after {lens[r]} max-abs {err:.3e}")
+    gs.close()
+    os_.close()

@@ -1,0 +1,80 @@
+// tools/gemm_splitk_bench.hip — prefill GEMM variants on the BLOOM prefill shapes (M tokens x N x K), HIP events,
+// median of 20 launches each: the library's dispatch (launch_linear), the round-2 tiles (64x64 / 64x32, 4-deep
+// ring) and 128x128 tiles with split-K KS = 1, 2, 3, 4, 6.  Every split-K output is checked against KS = 1 (the
+// same products summed in another order: max relative difference printed); gemm_mfma3 (128x128 tiles on
+// v_mfma_f32_32x32x16_bf16) at KS = 1, 2, 3, 4, 6, 8.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/gemm_splitk_bench.hip -o tools/gemm_splitk_bench
+#include "../distributed_inference_demo_amd/csrc/kernels.hip"
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+__global__ void fill_rand(bf16* p, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = d_lb32((uint32_t)i ^ seed);
+    p[i] = (bf16)(((float)(h >> 8) / 16777216.0f - 0.5f) * 0.5f);
+  }
+}
+
+int main() {
+  struct Sh { const char* name; int M, N, K; } shapes[] = {
+      {"1b1 qkv", 512, 4608, 1536}, {"1b1 dense", 512, 1536, 1536}, {"1b1 fc1", 512, 6144, 1536},
+      {"1b1 fc2", 512, 1536, 6144}, {"7b1 qkv", 512, 12288, 4096}, {"7b1 dense", 512, 4096, 4096},
+      {"7b1 fc1", 512, 16384, 4096}, {"7b1 fc2", 512, 4096, 16384}, {"3b dense B2", 1024, 2560, 2560}};
+  bf16 *X, *W, *bias; float *out, *ref, *resid, *ws; unsigned* tick;
+  CK(hipMalloc(&X, (size_t)1024 * 16384 * 2)); CK(hipMalloc(&W, (size_t)16384 * 16384 * 2));
+  CK(hipMalloc(&bias, 65536 * 2)); CK(hipMalloc(&out, (size_t)1024 * 16384 * 4)); CK(hipMalloc(&ref, (size_t)1024 * 16384 * 4));
+  CK(hipMalloc(&resid, (size_t)1024 * 16384 * 4)); CK(hipMemset(resid, 0, (size_t)1024 * 16384 * 4));
+  const size_t cap = (size_t)480 * 128 * 128;
+  CK(hipMalloc(&ws, cap * 4)); CK(hipMalloc(&tick, 4096 * 4)); CK(hipMemset(tick, 0, 4096 * 4));
+  fill_rand<<<4096, 256>>>(X, (size_t)1024 * 16384, 1); fill_rand<<<4096, 256>>>(W, (size_t)16384 * 16384, 2);
+  fill_rand<<<64, 256>>>(bias, 65536, 3);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (auto& sh : shapes) {
+    const int M = sh.M, N = sh.N, K = sh.K;
+    Epi ep{};
+    ep.kind = EPI_RESID; ep.bias = bias; ep.out_f32 = out; ep.resid = resid; ep.ldo = N;
+    ep.sk_ws = ws; ep.sk_tickets = tick; ep.sk_cap = cap; ep.sk_ntickets = 4096;
+    auto timeit = [&](auto&& fn) {
+      std::vector<float> t;
+      for (int it = 0; it < 25; it++) {
+        CK(hipEventRecord(e0)); fn(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        if (it >= 5) t.push_back(ms * 1e3f);
+      }
+      std::sort(t.begin(), t.end());
+      return t[t.size() / 2];
+    };
+    const double fl = 2.0 * M * N * K;
+    auto line = [&](const char* v, float us) {
+      printf("%-10s M=%4d N=%5d K=%5d  %-22s %8.2f us  %6.1f TFLOP/s  %.3f of 2500\n", sh.name, M, N, K, v, us,
+             fl / us * 1e-6, fl / us * 1e-6 / 2500);
+    };
+    line("launch_linear", timeit([&] { launch_linear(1, X, W, M, N, K, ep, 0); }));
+    // reference output: 64x32, KS = 1
+    gemm2_launch<64, 32, 4>(X, W, M, N, K, ep, 0, 1);
+    CK(hipMemcpy(ref, out, (size_t)M * N * 4, hipMemcpyDeviceToDevice));
+    std::vector<float> hr((size_t)M * N), ho((size_t)M * N);
+    CK(hipMemcpy(hr.data(), ref, hr.size() * 4, hipMemcpyDeviceToHost));
+    auto variant = [&](const char* tile, int bm, int bn, int ks, auto&& fn) {
+      const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+      if (K % (ks * 64) || (size_t)tiles * ks * bm * bn > cap || tiles > 4096) return;
+      char nm[64];
+      snprintf(nm, sizeof nm, "%s KS=%d (%ld)", tile, ks, tiles * ks);
+      const float us = timeit(fn);
+      CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (size_t i = 0; i < ho.size(); i++) md = std::max(md, (double)fabsf(ho[i] - hr[i]));
+      line(nm, us);
+      if (md > 1e-4) printf("           MISMATCH max |diff| %.3g\n", md);
+    };
+    for (int ks : {1, 4})
+      variant("64x64 r4", 64, 64, ks, [&] { gemm2_launch<64, 64, 4>(X, W, M, N, K, ep, 0, ks); });
+    for (int ks : {1, 2, 3, 4})
+      variant("128x128 m32 ps2", 128, 128, ks, [&] { gemm3_launch<2>(X, W, M, N, K, ep, 0, ks); });
+  }
+  return 0;
+}
