@@ -1577,17 +1577,31 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
 // ------------------------------------------------------------------------------------
 // gemm_mfma3: prefill GEMM on v_mfma_f32_32x32x16_bf16 (measured 2184 TFLOP/s against 1272 for the 16x16x32
 // form, bs_mfma_probe).  128 x 128 tile, 256 threads as 2 x 2 waves of 64 x 64 (2 x 2 accumulators of
-// 32 x 32), BK = 64, LDS double buffer (one __shared__ array) fed from a 2-deep register ring.  A wave
-// reads 16 KB of fragments per 64 K-columns for 262 K MACs: half the LDS bytes per MAC of the 64 x 64
-// tile's 32 x 32 waves, and a quarter of the MFMA instructions.  At prefill sizes the tile count is small (bloom-1b1 QKV at 512 tokens:
-// 144 tiles), so K is split over gridDim.z = KS blocks (fragment-order fp32 slabs, write-through, the
-// last-arriving block of a tile sums them in z order: deterministic whichever block arrives last).
+// 32 x 32), BK = 64, LDS double buffer (one __shared__ array) fed from a PS-deep register ring.  A wave reads
+// 16 KB of fragments per 64 K-columns for 262 K MACs: half the LDS bytes per MAC of the 64 x 64 tile's
+// 32 x 32 waves, and a quarter of the MFMA instructions.
+// Stream-K work split: at prefill sizes the tile count is small and uneven against 256 CUs (bloom-1b1 QKV
+// at 512 tokens: 144 tiles x 24 K-steps), so the tiles x K-steps iteration space is cut into gridDim.x equal
+// contiguous ranges, one per block.  A block runs the tile segments its range covers; a whole tile goes
+// straight to the epilogue, a partial one stores its fp32 fragments (write-through, slab 2 b + 0 for the
+// block's first segment, 2 b + 1 for its last) and takes the tile's ticket; the block drawing the last
+// ticket sums the tile's segments in K order (whichever block arrives last: deterministic) and runs the
+// epilogue.  Measured per block (tools/gemm3_stamps.hip): a 64-deep K-step costs ~0.67 us at one block per
+// CU, the prologue ~1.3 us, the LDS-staged epilogue ~3 us.
 // Fragment maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) holds A[row r][k 8h + j]
 // = X[m][k] and B[k 8h + j][col r] = W[n][k]; accumulator register e is row (e & 3) + 8 (e >> 2) + 4 h,
 // column r.  LDS rows are 128 B with the 16-B chunk index XOR-swizzled by (row >> 1) & 7: the 16 lanes
 // of a ds_read_b128 pass (rows 2k, 2k + 1 in the two halves of a 256-B bank row) hit 16 distinct slots.
 // ------------------------------------------------------------------------------------
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+#ifdef GEMM3_STAMPS
+__device__ unsigned long long g_gemm3_stamps[4096 * 4];
+#endif
+
+// Stream-K geometry shared by the kernel and the host: block bb's first iteration, and the block owning
+// iteration x (the largest bb with first(bb) <= x).
+__host__ __device__ __forceinline__ long gemm3_first(int bb, long T, int G) { return (long)bb * T / G; }
+__host__ __device__ __forceinline__ int gemm3_owner(long x, long T, int G) { return (int)(((x + 1) * G + T - 1) / T - 1); }
 
 template <int EK, int PS>
 __global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
@@ -1597,212 +1611,276 @@ __global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict_
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * BK];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1, r = lane & 31, h = lane >> 5;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int KS = gridDim.z, kz = blockIdx.z, Kz = K / KS;
+  const int tiles_n = (N + BN - 1) / BN, nk = K / BK;
+  const long T = (long)tiles_n * ((M + BM - 1) / BM) * nk;
+  const int G = gridDim.x, b = blockIdx.x;
+  const long it_begin = gemm3_first(b, T, G), it_end = gemm3_first(b + 1, T, G);
+#ifdef GEMM3_STAMPS
+  const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long st1 = 0, st2 = 0;
+#endif
   auto sw = [](int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); };
   auto As = [&](int buf) { return smem + buf * (BM + BN) * BK; };
   auto Bs = [&](int buf) { return smem + buf * (BM + BN) * BK + BM * BK; };
-
   // buffer loads: a 32-bit byte offset per lane and the K position as the scalar offset (the host checks
   // M * K and N * K bf16 fit 4 GB)
   const __amdgpu_buffer_rsrc_t rx = attn_rsrc(X), rw = attn_rsrc(W);
-  uint32_t oa[CA], ob[CB];
   int la[CA];
 #pragma unroll
   for (int i = 0; i < CA; i++) {
-    const int c = tid + i * 256, row = c >> 3, ch = c & 7;
-    oa[i] = (uint32_t)(((size_t)min(m0 + row, M - 1) * K + (size_t)kz * Kz + ch * 8) * 2);
-    ob[i] = (uint32_t)(((size_t)min(n0 + row, N - 1) * K + (size_t)kz * Kz + ch * 8) * 2);
-    la[i] = sw(row, ch);
+    const int c = tid + i * 256;
+    la[i] = sw(c >> 3, c & 7);
   }
-  float bias[2], cscale[2];
-#pragma unroll
-  for (int j = 0; j < 2; j++) {
-    const int n = min(n0 + wn * 64 + j * 32 + r, N - 1);
-    bias[j] = EK == EPI_ARGMAX ? 0.f : to_f32(((const bf16*)ep.bias)[n]);
-    cscale[j] = ep.col_scale ? ep.col_scale[n] : 1.f;
-  }
-  const int nk = Kz / BK;
-  bf16x8 ra[PS][CA], rb[PS][CB];
-  auto gload = [&](int st, int kt) {  // tile kt -> register stage st (clamped: a re-read past the end is unused)
-#ifdef GEMM3_ABLATE_LOADS
-    if (kt >= PS) return;
-#endif
-    const int off = min(kt, nk - 1) * BK * 2;
-#pragma unroll
-    for (int i = 0; i < CA; i++) ra[st][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, oa[i], off, 0));
-#pragma unroll
-    for (int i = 0; i < CB; i++) rb[st][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ob[i], off, 0));
+  const __amdgpu_buffer_rsrc_t rs = attn_rsrc(ep.sk_ws);
+  auto slab_off = [&](int slab, int i, int j, int q) {
+    return (uint32_t)(((((((size_t)slab * 4 + w) * 2 + i) * 2 + j) * 4 + q) * 64 + lane) * 16);
   };
-  auto lstore = [&](int st, int buf) {
-#pragma unroll
-    for (int i = 0; i < CA; i++) *reinterpret_cast<bf16x8*>(As(buf) + la[i]) = ra[st][i];
-#pragma unroll
-    for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(Bs(buf) + la[i]) = rb[st][i];
-  };
+  int* flag = reinterpret_cast<int*>(smem);
   f32x16 acc[2][2];
+
+  for (long it = it_begin; it < it_end;) {
+    const int t = (int)(it / nk), k0 = (int)(it - (long)t * nk);
+    const int kn = (int)min((long)(nk - k0), it_end - it);  // K-steps of this segment
+    const int tm = t / tiles_n, m0 = tm * BM, n0 = (t - tm * tiles_n) * BN;
+    const bool first_seg = it == it_begin;
+    it += kn;
+    uint32_t oa[CA], ob[CB];
 #pragma unroll
-  for (int i = 0; i < 2; i++)
+    for (int i = 0; i < CA; i++) {
+      const int c = tid + i * 256, row = c >> 3, ch = c & 7;
+      oa[i] = (uint32_t)(((size_t)min(m0 + row, M - 1) * K + (size_t)k0 * BK + ch * 8) * 2);
+      ob[i] = (uint32_t)(((size_t)min(n0 + row, N - 1) * K + (size_t)k0 * BK + ch * 8) * 2);
+    }
+    float bias[2], cscale[2];
 #pragma unroll
-    for (int j = 0; j < 2; j++)
+    for (int j = 0; j < 2; j++) {
+      const int n = min(n0 + wn * 64 + j * 32 + r, N - 1);
+      bias[j] = to_f32(((const bf16*)ep.bias)[n]);
+      cscale[j] = ep.col_scale ? ep.col_scale[n] : 1.f;
+    }
+    bf16x8 ra[PS][CA], rb[PS][CB];
+    auto gload = [&](int st, int kt) {  // segment step kt -> register stage st (clamped: a re-read past the end is unused)
+#ifdef GEMM3_ABLATE_LOADS
+      if (kt >= PS) return;
+#endif
+      const int off = min(kt, kn - 1) * BK * 2;
 #pragma unroll
-      for (int e = 0; e < 16; e++) acc[i][j][e] = 0.f;
-  auto ktile = [&](int buf) {
+      for (int i = 0; i < CA; i++) ra[st][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, oa[i], off, 0));
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ks++) {
-      bf16x8 af[2], bfr[2];
+      for (int i = 0; i < CB; i++) rb[st][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ob[i], off, 0));
+    };
+    auto lstore = [&](int st, int buf) {
 #pragma unroll
-      for (int i = 0; i < 2; i++) af[i] = *reinterpret_cast<const bf16x8*>(As(buf) + sw(wm * 64 + i * 32 + r, ks * 2 + h));
+      for (int i = 0; i < CA; i++) *reinterpret_cast<bf16x8*>(As(buf) + la[i]) = ra[st][i];
 #pragma unroll
-      for (int j = 0; j < 2; j++) bfr[j] = *reinterpret_cast<const bf16x8*>(Bs(buf) + sw(wn * 64 + j * 32 + r, ks * 2 + h));
+      for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(Bs(buf) + la[i]) = rb[st][i];
+    };
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int e = 0; e < 16; e++) acc[i][j][e] = 0.f;
+    auto ktile = [&](int buf) {
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ks++) {
+        bf16x8 af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++) af[i] = *reinterpret_cast<const bf16x8*>(As(buf) + sw(wm * 64 + i * 32 + r, ks * 2 + h));
+#pragma unroll
+        for (int j = 0; j < 2; j++) bfr[j] = *reinterpret_cast<const bf16x8*>(Bs(buf) + sw(wn * 64 + j * 32 + r, ks * 2 + h));
 #ifdef GEMM3_ABLATE_MFMA
-      acc[0][0][0] += (float)af[0][0] + (float)af[1][1] + (float)bfr[0][2] + (float)bfr[1][3];
+        acc[0][0][0] += (float)af[0][0] + (float)af[1][1] + (float)bfr[0][2] + (float)bfr[1][3];
 #else
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+          for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+#endif
+      }
+    };
+    // the ring of gemm_mfma2: full groups of PS steps run with no conditions, so the loads are counted
+    // with vmcnt(N); the previous segment's epilogue ended with a barrier, so the LDS is free
+#pragma unroll
+    for (int st = 0; st < PS; st++) gload(st, st);
+    lstore(0, 0);
+    gload(0, PS);
+    __syncthreads();
+#ifdef GEMM3_STAMPS
+    if (first_seg) st1 = __builtin_amdgcn_s_memrealtime();
+#endif
+    int cur = 0, kt0 = 0;
+    for (; kt0 + PS <= kn; kt0 += PS) {
+#pragma unroll
+      for (int s2 = 0; s2 < PS; s2++) {
+        const int kt = kt0 + s2, nst = (s2 + 1) % PS;
+        ktile(cur);
+        lstore(nst, cur ^ 1);
+        gload(nst, kt + 1 + PS);
+        __syncthreads();
+        cur ^= 1;
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < PS; s2++) {  // tail: kn % PS steps
+      const int kt = kt0 + s2, nst = (s2 + 1) % PS;
+      if (kt < kn) {
+        ktile(cur);
+        lstore(nst, cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+      }
+    }
+#ifdef GEMM3_STAMPS
+    if (first_seg) st2 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (kn < nk) {
+      // partial tile: fragments out, ticket; the last arriver sums the tile's segments in K order
+      const int slab = 2 * b + (first_seg ? 0 : 1);
 #pragma unroll
       for (int i = 0; i < 2; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-#endif
-    }
-  };
-  // the ring of gemm_mfma2 (PS = 2): full groups run with no conditions, so the loads are counted with vmcnt(N)
+        for (int j = 0; j < 2; j++)
 #pragma unroll
-  for (int st = 0; st < PS; st++) gload(st, st);
-  lstore(0, 0);
-  gload(0, PS);
-  __syncthreads();
-  int cur = 0, kt0 = 0;
-  for (; kt0 + PS <= nk; kt0 += PS) {
-#pragma unroll
-    for (int s2 = 0; s2 < PS; s2++) {
-      const int kt = kt0 + s2, nst = (s2 + 1) % PS;
-      ktile(cur);
-      lstore(nst, cur ^ 1);
-      gload(nst, kt + 1 + PS);
+          for (int q = 0; q < 4; q++) {
+            const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs, slab_off(slab, i, j, q), 0, 16);
+          }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int b_first = gemm3_owner((long)t * nk, T, G), b_last = gemm3_owner((long)(t + 1) * nk - 1, T, G);
       __syncthreads();
-      cur ^= 1;
-    }
-  }
-#pragma unroll
-  for (int s2 = 0; s2 < PS; s2++) {  // tail: nk % PS steps
-    const int kt = kt0 + s2, nst = (s2 + 1) % PS;
-    if (kt < nk) {
-      ktile(cur);
-      lstore(nst, cur ^ 1);
+      if (tid == 0) {
+        typedef __attribute__((address_space(1))) unsigned gu32;
+        const unsigned old = __hip_atomic_fetch_add((gu32*)(ep.sk_tickets + t), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (unsigned)(b_last - b_first);
+        if (last) __hip_atomic_store((gu32*)(ep.sk_tickets + t), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last;
+      }
       __syncthreads();
-      cur ^= 1;
+      const int is_last = *flag;
+      __syncthreads();  // the flag word is LDS the next segment overwrites
+      if (!is_last) continue;
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          f32x4 sum[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+          for (int bb = b_first; bb <= b_last; bb++) {
+            const int sl = 2 * bb + (gemm3_first(bb, T, G) >= (long)t * nk ? 0 : 1);
+            f32x4 v[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, slab_off(sl, i, j, q), 0, 16));
+#pragma unroll
+            for (int q = 0; q < 4; q++) sum[q] += v[q];
+          }
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) acc[i][j][4 * q + e] = sum[q][e];
+        }
     }
-  }
-  if (KS > 1) {
-    const size_t tile = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-    const __amdgpu_buffer_rsrc_t rs = attn_rsrc(ep.sk_ws + tile * KS * (BM * BN));
-    auto off = [&](int z, int i, int j, int q) { return (uint32_t)((((((z * 4 + w) * 2 + i) * 2 + j) * 4 + q) * 64 + lane) * 16); };
+    // Epilogue through LDS (the staging buffers are dead): each 64-row half of the tile is written there as
+    // fp32 (acc * col_scale + bias; row stride 136 floats, so the two lane halves of a store hit disjoint
+    // banks), then read back as 8-column chunks: one 16-B bf16 store (GELU, QKV) or two 16-B fp32 loads +
+    // stores (RESID) per chunk instead of 64 per-element accesses per lane.  The residual chunks and the
+    // rows' cached lengths of a half are loaded before its staging (clamped, unconditional: one round trip).
+    constexpr int SLD = 136;
+    float* stg = reinterpret_cast<float*>(smem);
+    auto chunk_rc = [&](int half, int c, int& lr, int& lc) { const int id = tid + c * 256; lr = half * 64 + (id >> 4); lc = (id & 15) * 8; };
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int half = 0; half < 2; half++) {
+      f32x4 rsd[4][2];
+      int cpast[4];
 #pragma unroll
-      for (int j = 0; j < 2; j++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs, off(kz, i, j, q), 0, 16);
+      for (int c = 0; c < 4; c++) {
+        int lr, lc;
+        chunk_rc(half, c, lr, lc);
+        const int m = min(m0 + lr, M - 1), n = min(n0 + lc, N - 8);
+        if constexpr (EK == EPI_RESID) {
+          rsd[c][0] = *reinterpret_cast<const f32x4*>(ep.resid + (size_t)m * ep.ldo + n);
+          rsd[c][1] = *reinterpret_cast<const f32x4*>(ep.resid + (size_t)m * ep.ldo + n + 4);
         }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);  // the LDS tiles are dead: the flag rides in the one array
-    if (tid == 0) {
-      typedef __attribute__((address_space(1))) unsigned gu32;
-      const unsigned old = __hip_atomic_fetch_add((gu32*)(ep.sk_tickets + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == (unsigned)(KS - 1);
-      if (last) __hip_atomic_store((gu32*)(ep.sk_tickets + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = last;
-    }
-    __syncthreads();
-    if (!*flag) return;
-    // every slab (this block's too) re-read unconditionally and summed in z order
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        f32x4 t[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-        for (int z = 0; z < KS; z++) {
-          f32x4 v[4];
-#pragma unroll
-          for (int q = 0; q < 4; q++) v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off(z, i, j, q), 0, 16));
-#pragma unroll
-          for (int q = 0; q < 4; q++) t[q] += v[q];
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-#pragma unroll
-          for (int e = 0; e < 4; e++) acc[i][j][4 * q + e] = t[q][e];
+        if constexpr (EK == EPI_QKV) cpast[c] = ep.past_dev ? ep.past_dev[m / ep.seq] : ep.past;
       }
-  }
-  // epilogue: per accumulator, its 16 per-element / per-row operands are loaded in one batch (clamped,
-  // unconditional: a guarded load per element would wait for each in turn), then the stores
-  auto row_of = [&](int i, int e) { return m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h; };
-  auto col_of = [&](int j) { return n0 + wn * 64 + j * 32 + r; };
-  if constexpr (EK == EPI_RESID) {
+      if (wm == half) {
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+        for (int i = 0; i < 2; i++)
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
-        float rsd[16];
+          for (int j = 0; j < 2; j++)
 #pragma unroll
-        for (int e = 0; e < 16; e++) rsd[e] = ep.resid[(size_t)min(row_of(i, e), M - 1) * ep.ldo + min(col_of(j), N - 1)];
-#pragma unroll
-        for (int e = 0; e < 16; e++) {
-          const int m = row_of(i, e), n = col_of(j);
-          if (m < M && n < N) ep.out_f32[(size_t)m * ep.ldo + n] = acc[i][j][e] * cscale[j] + bias[j] + rsd[e];
-        }
+            for (int e = 0; e < 16; e++)
+              stg[(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * SLD + wn * 64 + j * 32 + r] = acc[i][j][e] * cscale[j] + bias[j];
       }
-  } else if constexpr (EK == EPI_GELU) {
+      __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+      for (int c = 0; c < 4; c++) {
+        int lr, lc;
+        chunk_rc(half, c, lr, lc);
+        const int m = m0 + lr, n = n0 + lc;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + (lr - half * 64) * SLD + lc);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + (lr - half * 64) * SLD + lc + 4);
+        if (m >= M || n >= N) continue;
+        if constexpr (EK == EPI_RESID) {
+          float* o = ep.out_f32 + (size_t)m * ep.ldo + n;
+          *reinterpret_cast<f32x4*>(o) = v0 + rsd[c][0];
+          *reinterpret_cast<f32x4*>(o + 4) = v1 + rsd[c][1];
+        } else {
+          bf16x8 b8;
 #pragma unroll
-      for (int j = 0; j < 2; j++)
-#pragma unroll
-        for (int e = 0; e < 16; e++) {
-          const int m = row_of(i, e), n = col_of(j);
-          if (m < M && n < N)
-            ((bf16*)ep.out_act)[(size_t)m * ep.ldo + n] = from_f32<bf16>(gelu_bloom(acc[i][j][e] * cscale[j] + bias[j]));
-        }
-  } else if constexpr (EK == EPI_QKV) {
-    const int three = 3 * ep.head_dim;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      int past[16];
-#pragma unroll
-      for (int e = 0; e < 16; e++) past[e] = ep.past_dev ? ep.past_dev[min(row_of(i, e), M - 1) / ep.seq] : ep.past;
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        const int n = col_of(j);
-        const int head = n / three, rr = n - head * three, which = rr / ep.head_dim, d = rr - which * ep.head_dim;
-#pragma unroll
-        for (int e = 0; e < 16; e++) {
-          const int m = row_of(i, e);
-          if (m >= M || n >= N) continue;
-          const bf16 v = from_f32<bf16>(acc[i][j][e] * cscale[j] + bias[j]);
-          if (which == 0) {
-            ((bf16*)ep.q_out)[(size_t)m * ep.hidden + head * ep.head_dim + d] = v;
+          for (int q = 0; q < 4; q++) {
+            b8[q] = from_f32<bf16>(EK == EPI_GELU ? gelu_bloom(v0[q]) : v0[q]);
+            b8[4 + q] = from_f32<bf16>(EK == EPI_GELU ? gelu_bloom(v1[q]) : v1[q]);
+          }
+          if constexpr (EK == EPI_GELU) {
+            *reinterpret_cast<bf16x8*>((bf16*)ep.out_act + (size_t)m * ep.ldo + n) = b8;
           } else {
-            const int b = m / ep.seq, t = m - b * ep.seq;
-            const size_t idx = (((size_t)(ep.slot + b) * ep.n_head + head) * ep.max_ctx + past[e] + t) * ep.head_dim + d;
-            ((bf16*)(which == 1 ? ep.k_cache : ep.v_cache))[idx] = v;
+            const int three = 3 * ep.head_dim;
+            const int head = n / three, rr = n - head * three, which = rr / ep.head_dim, d = rr - which * ep.head_dim;
+            bf16* dst;
+            if (which == 0) {
+              dst = (bf16*)ep.q_out + (size_t)m * ep.hidden + head * ep.head_dim + d;
+            } else {
+              const int bi = m / ep.seq, ti = m - bi * ep.seq;
+              dst = (bf16*)(which == 1 ? ep.k_cache : ep.v_cache) +
+                    (((size_t)(ep.slot + bi) * ep.n_head + head) * ep.max_ctx + cpast[c] + ti) * ep.head_dim + d;
+            }
+            *reinterpret_cast<bf16x8*>(dst) = b8;
           }
         }
       }
+      __syncthreads();  // the staging rows are overwritten next (second half, or the next segment's tiles)
     }
   }
+#ifdef GEMM3_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();
+  if (tid < 4 && b < 4096) g_gemm3_stamps[b * 4 + tid] = tid == 0 ? st0 : tid == 1 ? st1 : tid == 2 ? st2 : st3;
+#endif
 }
 
-// gemm_mfma3_kernel launch: K % (KS * 64) == 0; KS > 1 needs ep.sk_ws / sk_tickets room (gemm3_split_k).
+// Grid of gemm_mfma3 (0: use another kernel).  Measured per-block costs (~1.3 us prologue, ~3 us epilogue,
+// ~0.67 us per 64-deep K-step at one block per CU) decide where it beats the 64 x 64 / 128 x 128 gemm_mfma2
+// tiles (profiles/r03_gemm3.txt): long K per block and at least ~256 blocks.  The grid is tiles x KS with
+// KS in {1, 2}, so the stream-K ranges fall on whole tiles (KS = 1, no partials) or tile halves.
+// Conditions: K % (64 KS) == 0, K / KS >= 2048, N % 8 == 0, QKV head_dim % 8 == 0, operands under 4 GB
+// (32-bit buffer offsets), partial slabs (2 per block, 64 KB each) in the workspace, one ticket per tile.
+static int gemm3_grid(int M, int N, int K, const Epi& ep) {
+  if (K % 64 || N % 8 || ep.kind == EPI_ARGMAX) return 0;
+  if (ep.kind == EPI_QKV && ep.head_dim % 8) return 0;
+  if ((size_t)M * K * 2 >= (1ull << 32) || (size_t)N * K * 2 >= (1ull << 32)) return 0;
+  const long tiles = (long)((M + 127) / 128) * ((N + 127) / 128);
+  const int ks = tiles >= 240 ? 1 : 2;
+  if (K % (64 * ks) || K / ks < 2048 || tiles * ks < 240) return 0;
+  if (ks > 1 && (!ep.sk_ws || !ep.sk_tickets || tiles > ep.sk_ntickets || (size_t)2 * tiles * ks * 128 * 128 > ep.sk_cap)) return 0;
+  return (int)(tiles * ks);
+}
+
 template <int PS = 2>
-static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int KS) {
-  dim3 grid((N + 127) / 128, (M + 127) / 128, KS);
+static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int G) {
   switch (ep.kind) {
-    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, PS><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
-    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, PS><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
-    default: gemm_mfma3_kernel<EPI_GELU, PS><<<grid, 256, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, PS><<<G, 256, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, PS><<<G, 256, 0, s>>>(x, w, M, N, K, ep); break;
+    default: gemm_mfma3_kernel<EPI_GELU, PS><<<G, 256, 0, s>>>(x, w, M, N, K, ep); break;
   }
 }
 
@@ -2050,7 +2128,10 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
   if ((K % 64) == 0) {
     // 128x128 when it still gives every CU a block (>= 240 blocks), else 64x64, else 64x32
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-    if (blocks(128, 128) >= 240) {
+    if (const int g3 = gemm3_grid(M, N, K, ep)) {
+      // long-K shapes with >= 240 128 x 128 work items (bloom-7b1 and wider at prefill sizes)
+      gemm3_launch<2>(x, w, M, N, K, ep, s, g3);
+    } else if (blocks(128, 128) >= 240) {
       gemm2_launch<128, 128, 1>(x, w, M, N, K, ep, s);
     } else if (blocks(64, 64) >= 128) {
       // below 240 128x128 tiles the K loop is latency-bound: 64x64 tiles with a 4-deep ring (beat 128x64,

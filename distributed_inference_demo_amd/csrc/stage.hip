@@ -72,8 +72,9 @@ struct ProfClass {
 // Split-K workspace of the batched decode GEMV (kernels.hip gemv_tiles_dispatch): up to 16 splits
 // of 32 rows x 4096 columns, one ticket per 16-column tile.  Used only by enqueue_forward's GEMVs
 // (one stream per stage); head slices on another stream never split K.
-// Also the prefill GEMM's split-K partials (kernels.hip gemm_split_k: at most ~480 128x128 tiles' worth).
-constexpr size_t kSkCap = (size_t)480 * 128 * 128;
+// Also the prefill GEMMs' partials: gemm_mfma3's stream-K slabs (2 per block of a grid of up to 512) and
+// gemm_split_k's 64x64 split-K tiles.
+constexpr size_t kSkCap = (size_t)1024 * 128 * 128;
 constexpr int kSkTickets = 4096;
 
 struct bs_stage {

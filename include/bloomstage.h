@@ -164,7 +164,10 @@ int bs_head_slice(bs_stage *stage, const void *xn, int32_t batch, const uint64_t
  *   = the first i whose running sum of w exceeds u * sum(w), u in [0, 1) from the stage's counter
  *   generator keyed by (seed, KV row, position): reproducible, unlike the reference's
  *   std::random_device seed (:61-63).  The reference never applies its temperature argument
- *   (:51-52); pass 1 to reproduce it.  Not available on vocabulary-slice (bs_head_slice) stages. */
+ *   (:51-52); pass 1 to reproduce it.  Not available on vocabulary-slice (bs_head_slice) stages.
+ *   The draw depends on nothing else: two requests decoded with the same seed in the same KV row
+ *   draw the same u at each position, so a server gives every request its own seed (for example
+ *   base_seed ^ request_id, set before the request's first sampled step). */
 int bs_set_sampling(bs_stage *stage, int32_t top_k, float temperature, uint64_t seed);
 
 /* ---- Decode engine ----

@@ -2,7 +2,7 @@
 // median of 20 launches each: the library's dispatch (launch_linear), the round-2 tiles (64x64 / 64x32, 4-deep
 // ring) and 128x128 tiles with split-K KS = 1, 2, 3, 4, 6.  Every split-K output is checked against KS = 1 (the
 // same products summed in another order: max relative difference printed); gemm_mfma3 (128x128 tiles on
-// v_mfma_f32_32x32x16_bf16) at KS = 1, 2, 3, 4, 6, 8.
+// v_mfma_f32_32x32x16_bf16, stream-K) at grids of 128..512 blocks.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/gemm_splitk_bench.hip -o tools/gemm_splitk_bench
 #include "../distributed_inference_demo_amd/csrc/kernels.hip"
 #include <algorithm>
@@ -27,7 +27,7 @@ int main() {
   CK(hipMalloc(&X, (size_t)1024 * 16384 * 2)); CK(hipMalloc(&W, (size_t)16384 * 16384 * 2));
   CK(hipMalloc(&bias, 65536 * 2)); CK(hipMalloc(&out, (size_t)1024 * 16384 * 4)); CK(hipMalloc(&ref, (size_t)1024 * 16384 * 4));
   CK(hipMalloc(&resid, (size_t)1024 * 16384 * 4)); CK(hipMemset(resid, 0, (size_t)1024 * 16384 * 4));
-  const size_t cap = (size_t)480 * 128 * 128;
+  const size_t cap = (size_t)1024 * 128 * 128;
   CK(hipMalloc(&ws, cap * 4)); CK(hipMalloc(&tick, 4096 * 4)); CK(hipMemset(tick, 0, 4096 * 4));
   fill_rand<<<4096, 256>>>(X, (size_t)1024 * 16384, 1); fill_rand<<<4096, 256>>>(W, (size_t)16384 * 16384, 2);
   fill_rand<<<64, 256>>>(bias, 65536, 3);
@@ -73,8 +73,16 @@ int main() {
     };
     for (int ks : {1, 4})
       variant("64x64 r4", 64, 64, ks, [&] { gemm2_launch<64, 64, 4>(X, W, M, N, K, ep, 0, ks); });
-    for (int ks : {1, 2, 3, 4})
-      variant("128x128 m32 ps2", 128, 128, ks, [&] { gemm3_launch<2>(X, W, M, N, K, ep, 0, ks); });
+    for (int G : {128, 192, 256, 384, 512}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "m32 stream-K G=%d", G);
+      const float us = timeit([&] { gemm3_launch<2>(X, W, M, N, K, ep, 0, G); });
+      CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (size_t i = 0; i < ho.size(); i++) md = std::max(md, (double)fabsf(ho[i] - hr[i]));
+      line(nm, us);
+      if (md > 1e-3) printf("           MISMATCH max |diff| %.3g\n", md);
+    }
   }
   return 0;
 }
