@@ -1576,18 +1576,18 @@ __global__ __launch_bounds__(256) void gemm_mfma2_kernel(const bf16* __restrict_
 
 // ------------------------------------------------------------------------------------
 // gemm_mfma3: prefill GEMM on v_mfma_f32_32x32x16_bf16 (measured 2184 TFLOP/s against 1272 for the 16x16x32
-// form, bs_mfma_probe).  128 x 128 tile, 256 threads as 2 x 2 waves of 64 x 64 (2 x 2 accumulators of
-// 32 x 32), BK = 64, LDS double buffer (one __shared__ array) fed from a PS-deep register ring.  A wave reads
-// 16 KB of fragments per 64 K-columns for 262 K MACs: half the LDS bytes per MAC of the 64 x 64 tile's
-// 32 x 32 waves, and a quarter of the MFMA instructions.
+// form, bs_mfma_probe).  128 x 128 tile, 512 threads as 2 x 4 waves of 64 x 32 (two 32 x 32 accumulators;
+// two waves per SIMD, so one's MFMAs run while the other waits on LDS), BK = 64.  Staging is LDS-DMA
+// (buffer_load ... lds: no VGPR round trip, no ds_write pass) into 3 LDS stages (96 KB): tile kt computes
+// while tiles kt + 1 and kt + 2 land, one raw s_barrier per step.
 // Stream-K work split: at prefill sizes the tile count is small and uneven against 256 CUs (bloom-1b1 QKV
 // at 512 tokens: 144 tiles x 24 K-steps), so the tiles x K-steps iteration space is cut into gridDim.x equal
 // contiguous ranges, one per block.  A block runs the tile segments its range covers; a whole tile goes
 // straight to the epilogue, a partial one stores its fp32 fragments (write-through, slab 2 b + 0 for the
 // block's first segment, 2 b + 1 for its last) and takes the tile's ticket; the block drawing the last
 // ticket sums the tile's segments in K order (whichever block arrives last: deterministic) and runs the
-// epilogue.  Measured per block (tools/gemm3_stamps.hip): a 64-deep K-step costs ~0.67 us at one block per
-// CU, the prologue ~1.3 us, the LDS-staged epilogue ~3 us.
+// epilogue (LDS-staged: 16-B stores).  Per block (tools/gemm3_stamps.hip, profiles/r03_gemm3_stamps*.txt):
+// ~0.52 us per 64-deep K-step, ~0.8 us prologue, ~2.5-3.5 us epilogue.
 // Fragment maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) holds A[row r][k 8h + j]
 // = X[m][k] and B[k 8h + j][col r] = W[n][k]; accumulator register e is row (e & 3) + 8 (e >> 2) + 4 h,
 // column r.  LDS rows are 128 B with the 16-B chunk index XOR-swizzled by (row >> 1) & 7: the 16 lanes
@@ -1604,13 +1604,15 @@ __host__ __device__ __forceinline__ long gemm3_first(int bb, long T, int G) { re
 __host__ __device__ __forceinline__ int gemm3_owner(long x, long T, int G) { return (int)(((x + 1) * G + T - 1) / T - 1); }
 
 template <int EK, int PS>
-__global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
+__global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                                          int M, int N, int K, Epi ep) {
   constexpr int BM = 128, BN = 128, BK = 64;
-  constexpr int CA = BM * BK / 8 / 256, CB = BN * BK / 8 / 256;  // 16-B chunks per thread per stage: 4, 4
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * BK];
+  constexpr int NTH = 512;                       // 8 waves: 2 per SIMD, one's MFMAs cover the other's LDS waits
+  constexpr int CA = BM * BK / 8 / NTH, CB = BN * BK / 8 / NTH;  // 16-B chunks per thread per stage: 2, 2
+  constexpr int NSTG = 3;                        // LDS stages: tile kt computes while kt + 1, kt + 2 land
+  __shared__ __attribute__((aligned(16))) bf16 smem[NSTG * (BM + BN) * BK];  // 96 KB, the only LDS object
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1, r = lane & 31, h = lane >> 5;
+  const int wm = w >> 2, wn = w & 3, r = lane & 31, h = lane >> 5;  // wave tile 64 x 32 at (64 wm, 32 wn)
   const int tiles_n = (N + BN - 1) / BN, nk = K / BK;
   const long T = (long)tiles_n * ((M + BM - 1) / BM) * nk;
   const int G = gridDim.x, b = blockIdx.x;
@@ -1622,21 +1624,17 @@ __global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict_
   auto sw = [](int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); };
   auto As = [&](int buf) { return smem + buf * (BM + BN) * BK; };
   auto Bs = [&](int buf) { return smem + buf * (BM + BN) * BK + BM * BK; };
-  // buffer loads: a 32-bit byte offset per lane and the K position as the scalar offset (the host checks
-  // M * K and N * K bf16 fit 4 GB)
+  // Staging: buffer loads straight into LDS (LDS-DMA, no VGPR round trip), a 32-bit byte offset per lane
+  // and the K position as the scalar offset (the host checks M * K and N * K bf16 fit 4 GB).  An LDS-DMA
+  // instruction writes 64 consecutive 16-B slots (wave-uniform base + 16 lane), so the XOR swizzle is
+  // applied on the global side: the lane filling slot s of row `row` fetches logical chunk s ^ f(row).
   const __amdgpu_buffer_rsrc_t rx = attn_rsrc(X), rw = attn_rsrc(W);
-  int la[CA];
-#pragma unroll
-  for (int i = 0; i < CA; i++) {
-    const int c = tid + i * 256;
-    la[i] = sw(c >> 3, c & 7);
-  }
   const __amdgpu_buffer_rsrc_t rs = attn_rsrc(ep.sk_ws);
   auto slab_off = [&](int slab, int i, int j, int q) {
-    return (uint32_t)(((((((size_t)slab * 4 + w) * 2 + i) * 2 + j) * 4 + q) * 64 + lane) * 16);
+    return (uint32_t)((((((size_t)slab * 8 + w) * 2 + i) * 4 + q) * 64 + lane) * 16);
   };
   int* flag = reinterpret_cast<int*>(smem);
-  f32x16 acc[2][2];
+  f32x16 acc[2][1];
 
   for (long it = it_begin; it < it_end;) {
     const int t = (int)(it / nk), k0 = (int)(it - (long)t * nk);
@@ -1647,90 +1645,72 @@ __global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict_
     uint32_t oa[CA], ob[CB];
 #pragma unroll
     for (int i = 0; i < CA; i++) {
-      const int c = tid + i * 256, row = c >> 3, ch = c & 7;
+      const int c = i * NTH + w * 64 + lane, row = c >> 3, ch = (c & 7) ^ ((row >> 1) & 7);
       oa[i] = (uint32_t)(((size_t)min(m0 + row, M - 1) * K + (size_t)k0 * BK + ch * 8) * 2);
       ob[i] = (uint32_t)(((size_t)min(n0 + row, N - 1) * K + (size_t)k0 * BK + ch * 8) * 2);
     }
-    float bias[2], cscale[2];
+    float bias[1], cscale[1];
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-      const int n = min(n0 + wn * 64 + j * 32 + r, N - 1);
+    for (int j = 0; j < 1; j++) {
+      const int n = min(n0 + wn * 32 + r, N - 1);
       bias[j] = to_f32(((const bf16*)ep.bias)[n]);
       cscale[j] = ep.col_scale ? ep.col_scale[n] : 1.f;
     }
-    bf16x8 ra[PS][CA], rb[PS][CB];
-    auto gload = [&](int st, int kt) {  // segment step kt -> register stage st (clamped: a re-read past the end is unused)
-#ifdef GEMM3_ABLATE_LOADS
-      if (kt >= PS) return;
-#endif
+    typedef __attribute__((address_space(3))) void lds_void;
+    auto gload = [&](int buf, int kt) {  // segment step kt -> LDS stage buf (clamped: a re-load past the end is unread)
       const int off = min(kt, kn - 1) * BK * 2;
 #pragma unroll
-      for (int i = 0; i < CA; i++) ra[st][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, oa[i], off, 0));
+      for (int i = 0; i < CA; i++)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void*)(As(buf) + (i * NTH + w * 64) * 8), 16, oa[i], off, 0, 0);
 #pragma unroll
-      for (int i = 0; i < CB; i++) rb[st][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ob[i], off, 0));
-    };
-    auto lstore = [&](int st, int buf) {
-#pragma unroll
-      for (int i = 0; i < CA; i++) *reinterpret_cast<bf16x8*>(As(buf) + la[i]) = ra[st][i];
-#pragma unroll
-      for (int i = 0; i < CB; i++) *reinterpret_cast<bf16x8*>(Bs(buf) + la[i]) = rb[st][i];
+      for (int i = 0; i < CB; i++)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(Bs(buf) + (i * NTH + w * 64) * 8), 16, ob[i], off, 0, 0);
     };
 #pragma unroll
     for (int i = 0; i < 2; i++)
 #pragma unroll
-      for (int j = 0; j < 2; j++)
+      for (int j = 0; j < 1; j++)
 #pragma unroll
         for (int e = 0; e < 16; e++) acc[i][j][e] = 0.f;
     auto ktile = [&](int buf) {
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ks++) {
-        bf16x8 af[2], bfr[2];
+        bf16x8 af[2], bfr[1];
 #pragma unroll
         for (int i = 0; i < 2; i++) af[i] = *reinterpret_cast<const bf16x8*>(As(buf) + sw(wm * 64 + i * 32 + r, ks * 2 + h));
-#pragma unroll
-        for (int j = 0; j < 2; j++) bfr[j] = *reinterpret_cast<const bf16x8*>(Bs(buf) + sw(wn * 64 + j * 32 + r, ks * 2 + h));
+        bfr[0] = *reinterpret_cast<const bf16x8*>(Bs(buf) + sw(wn * 32 + r, ks * 2 + h));
 #ifdef GEMM3_ABLATE_MFMA
-        acc[0][0][0] += (float)af[0][0] + (float)af[1][1] + (float)bfr[0][2] + (float)bfr[1][3];
+        acc[0][0][0] += (float)af[0][0] + (float)af[1][1] + (float)bfr[0][2];
 #else
 #pragma unroll
-        for (int i = 0; i < 2; i++)
-#pragma unroll
-          for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 2; i++) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[0], acc[i][0], 0, 0, 0);
 #endif
       }
     };
-    // the ring of gemm_mfma2: full groups of PS steps run with no conditions, so the loads are counted
-    // with vmcnt(N); the previous segment's epilogue ended with a barrier, so the LDS is free
-#pragma unroll
-    for (int st = 0; st < PS; st++) gload(st, st);
-    lstore(0, 0);
-    gload(0, PS);
-    __syncthreads();
+    // Step kt: this wave's DMA of tile kt retired (vmcnt(CA + CB) leaves tile kt + 1's in flight) ->
+    // barrier (every wave's part of tile kt has landed; every wave is done reading tile kt - 1) -> DMA of
+    // tile kt + 2 into tile kt - 1's stage -> MFMAs of tile kt.  One barrier per step, raw s_barrier: a
+    // __syncthreads() would also wait vmcnt(0) and drain the DMA in flight (cdna_hip_programming.md §5,
+    // "Pipelining across barriers").  The previous segment's epilogue ended with a barrier: the LDS is free.
+    gload(0, 0);
+    gload(1, 1);
 #ifdef GEMM3_STAMPS
     if (first_seg) st1 = __builtin_amdgcn_s_memrealtime();
 #endif
-    int cur = 0, kt0 = 0;
-    for (; kt0 + PS <= kn; kt0 += PS) {
-#pragma unroll
-      for (int s2 = 0; s2 < PS; s2++) {
-        const int kt = kt0 + s2, nst = (s2 + 1) % PS;
-        ktile(cur);
-        lstore(nst, cur ^ 1);
-        gload(nst, kt + 1 + PS);
-        __syncthreads();
-        cur ^= 1;
-      }
+    int buf = 0, nbuf = 2;  // stage of tile kt, stage for tile kt + 2
+    for (int kt = 0; kt < kn; kt++) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CA + CB) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      gload(nbuf, kt + 2);
+      ktile(buf);
+      buf = buf == NSTG - 1 ? 0 : buf + 1;
+      nbuf = nbuf == NSTG - 1 ? 0 : nbuf + 1;
     }
-#pragma unroll
-    for (int s2 = 0; s2 < PS; s2++) {  // tail: kn % PS steps
-      const int kt = kt0 + s2, nst = (s2 + 1) % PS;
-      if (kt < kn) {
-        ktile(cur);
-        lstore(nst, cur ^ 1);
-        __syncthreads();
-        cur ^= 1;
-      }
-    }
+    // the clamped DMAs past the end land before the LDS is reused (partials' flag, epilogue staging)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 #ifdef GEMM3_STAMPS
     if (first_seg) st2 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1740,7 +1720,7 @@ __global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict_
 #pragma unroll
       for (int i = 0; i < 2; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < 1; j++)
 #pragma unroll
           for (int q = 0; q < 4; q++) {
             const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
@@ -1763,7 +1743,7 @@ __global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict_
 #pragma unroll
       for (int i = 0; i < 2; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
+        for (int j = 0; j < 1; j++) {
           f32x4 sum[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
           for (int bb = b_first; bb <= b_last; bb++) {
             const int sl = 2 * bb + (gemm3_first(bb, T, G) >= (long)t * nk ? 0 : 1);
@@ -1786,13 +1766,13 @@ __global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict_
     // rows' cached lengths of a half are loaded before its staging (clamped, unconditional: one round trip).
     constexpr int SLD = 136;
     float* stg = reinterpret_cast<float*>(smem);
-    auto chunk_rc = [&](int half, int c, int& lr, int& lc) { const int id = tid + c * 256; lr = half * 64 + (id >> 4); lc = (id & 15) * 8; };
+    auto chunk_rc = [&](int half, int c, int& lr, int& lc) { const int id = tid + c * NTH; lr = half * 64 + (id >> 4); lc = (id & 15) * 8; };
 #pragma unroll
     for (int half = 0; half < 2; half++) {
-      f32x4 rsd[4][2];
-      int cpast[4];
+      f32x4 rsd[2][2];
+      int cpast[2];
 #pragma unroll
-      for (int c = 0; c < 4; c++) {
+      for (int c = 0; c < 2; c++) {
         int lr, lc;
         chunk_rc(half, c, lr, lc);
         const int m = min(m0 + lr, M - 1), n = min(n0 + lc, N - 8);
@@ -1806,14 +1786,12 @@ __global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict_
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
-          for (int j = 0; j < 2; j++)
-#pragma unroll
-            for (int e = 0; e < 16; e++)
-              stg[(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * SLD + wn * 64 + j * 32 + r] = acc[i][j][e] * cscale[j] + bias[j];
+          for (int e = 0; e < 16; e++)
+            stg[(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * SLD + wn * 32 + r] = acc[i][0][e] * cscale[0] + bias[0];
       }
       __syncthreads();
 #pragma unroll
-      for (int c = 0; c < 4; c++) {
+      for (int c = 0; c < 2; c++) {
         int lr, lc;
         chunk_rc(half, c, lr, lc);
         const int m = m0 + lr, n = n0 + lc;
@@ -1858,29 +1836,38 @@ __global__ __launch_bounds__(256) void gemm_mfma3_kernel(const bf16* __restrict_
 #endif
 }
 
-// Grid of gemm_mfma3 (0: use another kernel).  Measured per-block costs (~1.3 us prologue, ~3 us epilogue,
-// ~0.67 us per 64-deep K-step at one block per CU) decide where it beats the 64 x 64 / 128 x 128 gemm_mfma2
-// tiles (profiles/r03_gemm3.txt): long K per block and at least ~256 blocks.  The grid is tiles x KS with
-// KS in {1, 2}, so the stream-K ranges fall on whole tiles (KS = 1, no partials) or tile halves.
-// Conditions: K % (64 KS) == 0, K / KS >= 2048, N % 8 == 0, QKV head_dim % 8 == 0, operands under 4 GB
-// (32-bit buffer offsets), partial slabs (2 per block, 64 KB each) in the workspace, one ticket per tile.
+// Grid of gemm_mfma3 (0: use another kernel), from the per-block costs tools/gemm3_stamps.hip measured
+// (~0.8 us prologue, ~2.5-3.5 us epilogue, ~0.52 us per 64-deep K-step at one block per CU) and the sweeps
+// against gemm_mfma2 (profiles/r03_gemm3.txt): 256 blocks (one per CU, stream-K ranges over the tiles) when
+// there are >= 256 tiles; otherwise tiles x KS blocks with KS = 256 / tiles (at most 4) splitting K, taken only
+// when a block keeps >= 16 K-steps (short-K narrow shapes like bloom-1b1's dense stay on 64 x 64 tiles).
+// Conditions: K % 64 == 0, N % 8 == 0, QKV head_dim % 8 == 0, operands under 4 GB (32-bit buffer offsets),
+// partial slabs (2 per block, 64 KB each) in the workspace, one ticket per tile.
 static int gemm3_grid(int M, int N, int K, const Epi& ep) {
   if (K % 64 || N % 8 || ep.kind == EPI_ARGMAX) return 0;
   if (ep.kind == EPI_QKV && ep.head_dim % 8) return 0;
   if ((size_t)M * K * 2 >= (1ull << 32) || (size_t)N * K * 2 >= (1ull << 32)) return 0;
+  if (!ep.sk_ws || !ep.sk_tickets) return 0;
   const long tiles = (long)((M + 127) / 128) * ((N + 127) / 128);
-  const int ks = tiles >= 240 ? 1 : 2;
-  if (K % (64 * ks) || K / ks < 2048 || tiles * ks < 240) return 0;
-  if (ks > 1 && (!ep.sk_ws || !ep.sk_tickets || tiles > ep.sk_ntickets || (size_t)2 * tiles * ks * 128 * 128 > ep.sk_cap)) return 0;
-  return (int)(tiles * ks);
+  const long nk = K / 64;
+  long G;
+  if (tiles >= 256) {
+    G = 256;
+  } else {
+    const long ks = std::max(1L, std::min(4L, 256 / tiles));
+    if (nk / ks < 16) return 0;
+    G = tiles * ks;
+  }
+  if (tiles > ep.sk_ntickets || (size_t)2 * G * 128 * 128 > ep.sk_cap) return 0;
+  return (int)G;
 }
 
 template <int PS = 2>
 static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int G) {
   switch (ep.kind) {
-    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, PS><<<G, 256, 0, s>>>(x, w, M, N, K, ep); break;
-    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, PS><<<G, 256, 0, s>>>(x, w, M, N, K, ep); break;
-    default: gemm_mfma3_kernel<EPI_GELU, PS><<<G, 256, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, PS><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, PS><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    default: gemm_mfma3_kernel<EPI_GELU, PS><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
   }
 }
 
@@ -2129,7 +2116,6 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
     // 128x128 when it still gives every CU a block (>= 240 blocks), else 64x64, else 64x32
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
     if (const int g3 = gemm3_grid(M, N, K, ep)) {
-      // long-K shapes with >= 240 128 x 128 work items (bloom-7b1 and wider at prefill sizes)
       gemm3_launch<2>(x, w, M, N, K, ep, s, g3);
     } else if (blocks(128, 128) >= 240) {
       gemm2_launch<128, 128, 1>(x, w, M, N, K, ep, s);

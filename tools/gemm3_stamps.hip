@@ -22,9 +22,9 @@ static double med(std::vector<double> v) { std::sort(v.begin(), v.end()); return
 
 int main() {
   struct Sh { const char* name; int M, N, K, G, kind; } shapes[] = {
-      {"1b1 qkv", 512, 4608, 1536, 256, EPI_RESID}, {"1b1 qkv gelu-epi", 512, 4608, 1536, 256, EPI_GELU},
-      {"1b1 fc1", 512, 6144, 1536, 256, EPI_GELU}, {"1b1 fc2", 512, 1536, 6144, 256, EPI_RESID},
-      {"1b1 dense", 512, 1536, 1536, 256, EPI_RESID}, {"7b1 fc2", 512, 4096, 16384, 256, EPI_RESID}};
+      {"1b1 qkv", 512, 4608, 1536, 144, EPI_RESID}, {"1b1 fc1", 512, 6144, 1536, 192, EPI_GELU},
+      {"1b1 fc2 KS=4", 512, 1536, 6144, 192, EPI_RESID}, {"7b1 qkv", 512, 12288, 4096, 384, EPI_RESID},
+      {"7b1 fc2 KS=2", 512, 4096, 16384, 256, EPI_RESID}};
   bf16 *X, *W, *bias, *act; float *out, *resid, *ws; unsigned* tick;
   CK(hipMalloc(&X, (size_t)1024 * 16384 * 2)); CK(hipMalloc(&W, (size_t)16384 * 16384 * 2));
   CK(hipMalloc(&bias, 65536 * 2)); CK(hipMalloc(&out, (size_t)1024 * 16384 * 4)); CK(hipMalloc(&act, (size_t)1024 * 16384 * 2));
