@@ -253,15 +253,22 @@ def bench_single(args):
         stream = cs.cuda_stream
         ids = torch.from_numpy(_prompt(B, P, m.vocab)).to(dev)
         tok = torch.empty(B, dtype=torch.int32, device=dev)
-        # prefill (timed on its own, bracketed by syncs; eager with GEMM events)
+        # prefill: one untimed pass (first launch of every kernel), the timed pass (bracketed by syncs,
+        # no events), then a pass with HIP events around every GEMM for the GEMM/other split.  Every pass
+        # rewrites the same KV rows of slot 0 with the same values.
+        st.forward(ids, tok, B, P, slot=0, past_len=0, stream=stream)
         torch.cuda.synchronize()
-        st.profile_enable(0 if args.no_profile else 2)
         t0 = time.perf_counter()
         st.forward(ids, tok, B, P, slot=0, past_len=0, stream=stream)
         torch.cuda.synchronize()
         t_prefill = time.perf_counter() - t0
-        pf_ms, pf_n, pf_flops = st.profile_read()
-        st.profile_enable(0)
+        pf_ms = pf_n = pf_flops = 0
+        if not args.no_profile:
+            st.profile_enable(2)
+            st.forward(ids, tok, B, P, slot=0, past_len=0, stream=stream)
+            torch.cuda.synchronize()
+            pf_ms, pf_n, pf_flops = st.profile_read()
+            st.profile_enable(0)
         past = P
         for _ in range(W):  # warm-up (captures the decode graph)
             st.forward(tok, tok, B, 1, slot=0, past_len=past, stream=stream)
@@ -325,7 +332,10 @@ def bench_single(args):
     res["stage_hbm"] = {"algo_bytes_per_step": step_bytes, "achieved_GBps": step_bytes / (ms_step * 1e-3) / 1e9,
                         "frac_of_peak": step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     res["prefill"] = {"tokens": B * P, "ms": t_prefill * 1e3, "tokens_per_s": B * P / t_prefill,
-                      "algo_flops": config.prefill_flops(m, m.n_layer, B, P, True)}
+                      "algo_flops": config.prefill_flops(m, m.n_layer, B, P, True),
+                      "timing": "second of three identical prefills (the first warms every kernel), host clock "
+                                "between device syncs, no events; gemm_TFLOPs from HIP events around every "
+                                "GEMM in the third"}
     res["prefill"]["achieved_TFLOPs"] = res["prefill"]["algo_flops"] / t_prefill / 1e12
     if pf_n:
         res["prefill"]["gemm_TFLOPs"] = pf_flops / (pf_ms * 1e-3) / 1e12

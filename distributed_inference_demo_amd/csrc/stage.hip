@@ -138,6 +138,7 @@ struct bs_stage {
   char* eng_ws = nullptr;
   size_t eng_layer_bytes = 0;
   int eng_on = 0;                   // bs_set_decode_engine (off until it beats the launches)
+  int graphs_on = 1;                // bs_set_graphs: decode steps on device buffers replay captured graphs
   int eng_used = 0;                 // the last enqueued forward took the engine
 };
 
@@ -1274,13 +1275,14 @@ extern "C" int bs_debug_engine_sync(bs_stage* s, uint32_t* out, int32_t n) {
   return (int)(nb / 4);
 }
 
-static bool graphs_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("BS_NO_GRAPH");
-    on = !(e && *e && *e != '0');
-  }
-  return on != 0;
+extern "C" int bs_set_graphs(bs_stage* s, int32_t on) {
+  if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
+  HIP_TRY(hipSetDevice(s->d.device));
+  HIP_TRY(hipDeviceSynchronize());
+  for (auto& g : s->graphs) hipGraphExecDestroy(g.second);
+  s->graphs.clear();
+  s->graphs_on = on ? 1 : 0;
+  return BS_OK;
 }
 
 extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void* out, float* logits, void* stream) {
@@ -1316,7 +1318,7 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
   const bool past_matches = s->past_next_valid && s->past_stream == st && (int)s->past_next.size() == B &&
                             std::equal(pasts.begin(), pasts.end(), s->past_next.begin());
   s->past_next_valid = false;  // until this forward is enqueued
-  const bool graph = S == 1 && !host_io && s->prof.cls == 0 && graphs_enabled();
+  const bool graph = S == 1 && !host_io && s->prof.cls == 0 && s->graphs_on;
   if (graph) {
     GraphKey key{B, slot, step->flags, in, out, logits, st};
     hipGraphExec_t exec = nullptr;

@@ -82,7 +82,7 @@ EXPORTS = [
     "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
     "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice", "bs_stream_delay", "bs_set_sampling",
     "bs_build_id", "bs_hbm_probe", "bs_mfma_probe", "bs_init_stage_file", "bs_weights_file_probe",
-    "bs_set_decode_engine", "bs_engine_status",
+    "bs_set_decode_engine", "bs_engine_status", "bs_set_graphs",
 ]
 
 _LIB = None
@@ -135,6 +135,7 @@ def lib():
         L.bs_head_slice.argtypes = [vp, vp, i32, vp, vp, vp, vp]
         L.bs_set_sampling.argtypes = [vp, i32, ctypes.c_float, ctypes.c_uint64]
         L.bs_set_decode_engine.argtypes = [vp, i32]
+        L.bs_set_graphs.argtypes = [vp, i32]
         L.bs_engine_status.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.bs_hbm_probe.argtypes = [i32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.bs_mfma_probe.argtypes = [i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
@@ -244,8 +245,12 @@ class Stage:
         decoding.cpp:24-66's order (last stage only)."""
         _check(lib().bs_set_sampling(self._h, int(top_k), float(temperature), int(seed)))
 
+    def set_graphs(self, on=True):
+        """bs_set_graphs: replay captured decode graphs (default) or launch every step eagerly."""
+        _check(lib().bs_set_graphs(self._h, 1 if on else 0))
+
     def set_decode_engine(self, on=True):
-        """bs_set_decode_engine: the persistent decode engine (default on) or the per-block launches."""
+        """bs_set_decode_engine: the persistent decode engine (default off) or the per-block launches."""
         _check(lib().bs_set_decode_engine(self._h, 1 if on else 0))
 
     def engine_status(self):

@@ -170,6 +170,11 @@ int bs_head_slice(bs_stage *stage, const void *xn, int32_t batch, const uint64_t
  *   base_seed ^ request_id, set before the request's first sampled step). */
 int bs_set_sampling(bs_stage *stage, int32_t top_k, float temperature, uint64_t seed);
 
+/* Decode steps (S = 1) on device buffers are captured once per shape into a hipGraph and replayed
+ * (the default, on = 1); on = 0 launches them eagerly every step (same kernels, same results: for
+ * debugging and A/B timing).  Drops captured graphs.  Returns BS_OK. */
+int bs_set_graphs(bs_stage *stage, int32_t on);
+
 /* ---- Decode engine ----
  * bf16 stages of hidden 1024 or 1536 (bloom-560m / bloom-1b1 widths) run a decode step of <= 2 rows
  * (S = 1; contexts <= 1024 at one row, <= 512 at two) as ONE persistent launch of every decoder block

@@ -315,35 +315,27 @@ def test_graph_replayed_decode_matches_oracle_long_context(dtype):
 
 
 def test_graph_and_eager_paths_agree_bitwise():
-    """Replays of the captured decode graph give the same bits as the eager launch sequence."""
-    import subprocess
-    import sys
-    code = (
-        "import numpy as np, torch, sys\n"
-        "sys.path.insert(0, '.')\n"
-        "from distributed_inference_demo_amd.stage import Stage\n"
-        "from oracle import gen_np\n"
-        "st = Stage(256, 4, 2, 1024, 0, 2, max_batch=2, max_ctx=64, seed=5)\n"
-        "cs = torch.cuda.Stream()\n"
-        "with torch.cuda.stream(cs):\n"
-        "  ids = torch.from_numpy(gen_np.prompt_ids(3, 2, 10, 1024).astype(np.int32)).cuda()\n"
-        "  tok = torch.empty(2, dtype=torch.int32, device='cuda'); lg = torch.empty((2, 1024), device='cuda')\n"
-        "  st.forward(ids, tok, 2, 10, past_len=0, stream=cs.cuda_stream)\n"
-        "  out = []\n"
-        "  for i in range(20):\n"
-        "    st.forward(tok, tok, 2, 1, past_len=10 + i, logits=lg, stream=cs.cuda_stream); out.append(lg.cpu().numpy())\n"
-        "np.save(sys.argv[1], np.stack(out))\n")
-    import os
-    import tempfile
-    d = tempfile.mkdtemp()
-    env = dict(os.environ)
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for flag, name in (("0", "graph"), ("1", "eager")):
-        env["BS_NO_GRAPH"] = flag
-        subprocess.run([sys.executable, "-c", code, os.path.join(d, name + ".npy")], check=True, env=env, cwd=root,
-                       timeout=120)
-    a, b = np.load(os.path.join(d, "graph.npy")), np.load(os.path.join(d, "eager.npy"))
-    assert np.array_equal(a, b)
+    """Replays of the captured decode graph give the same bits as the eager launch sequence
+    (bs_set_graphs(0) on a twin stage): 20 decode steps of 2 rows, logits compared bit for bit."""
+    import torch
+    from oracle import gen_np
+    out = {}
+    for graphs in (True, False):
+        st = Stage(256, 4, 2, 1024, 0, 2, max_batch=2, max_ctx=64, seed=5)
+        st.set_graphs(graphs)
+        cs = torch.cuda.Stream()
+        with torch.cuda.stream(cs):
+            ids = torch.from_numpy(gen_np.prompt_ids(3, 2, 10, 1024).astype(np.int32)).cuda()
+            tok = torch.empty(2, dtype=torch.int32, device="cuda")
+            lg = torch.empty((2, 1024), device="cuda")
+            st.forward(ids, tok, 2, 10, past_len=0, stream=cs.cuda_stream)
+            steps = []
+            for i in range(20):
+                st.forward(tok, tok, 2, 1, past_len=10 + i, logits=lg, stream=cs.cuda_stream)
+                steps.append(lg.cpu().numpy())
+        st.close()
+        out[graphs] = np.stack(steps)
+    assert np.array_equal(out[True], out[False])
 
 
 def test_stream_switch_rewrites_positions():
