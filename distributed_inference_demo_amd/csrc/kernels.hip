@@ -1679,12 +1679,8 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
 #pragma unroll
         for (int i = 0; i < 2; i++) af[i] = *reinterpret_cast<const bf16x8*>(As(buf) + sw(wm * 64 + i * 32 + r, ks * 2 + h));
         bfr[0] = *reinterpret_cast<const bf16x8*>(Bs(buf) + sw(wn * 32 + r, ks * 2 + h));
-#ifdef GEMM3_ABLATE_MFMA
-        acc[0][0][0] += (float)af[0][0] + (float)af[1][1] + (float)bfr[0][2];
-#else
 #pragma unroll
         for (int i = 0; i < 2; i++) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[0], acc[i][0], 0, 0, 0);
-#endif
       }
     };
     // Step kt: this wave's DMA of tile kt retired (vmcnt(CA + CB) leaves tile kt + 1's in flight) ->
@@ -2712,7 +2708,10 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
     const int nsplit = attention_decode_splits(a.B, a.n_head, a.max_chunks);
     if (nsplit == 1) {
       dim3 g(a.n_head, a.B, 1);
-      if (is_bf16) attn_decode_kernel<bf16, 8><<<g, 512, 0, s>>>(a);
+      // the 8-wave block holds a CU (228 VGPRs: 2 waves per SIMD); above 256 (row, head) pairs, 4-wave
+      // blocks run two per CU, so the grid takes half the rounds (bloom-1b1 B = 32: 512 pairs)
+      if (is_bf16 && a.B * a.n_head > 256) attn_decode_kernel<bf16, 4><<<g, 256, 0, s>>>(a);
+      else if (is_bf16) attn_decode_kernel<bf16, 8><<<g, 512, 0, s>>>(a);
       else attn_decode_kernel<float, 8><<<g, 512, 0, s>>>(a);
     } else if (is_bf16 && a.defer_merge) {
       // few (row, head) pairs: 8 waves x 32 positions per block, half the serial work per wave

@@ -7,3 +7,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 timeout -k 10 400 python bench.py > gpurun_out/final_bench.json 2> gpurun_out/final_bench.err || exit 1
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/final_prof -o run --output-format csv -- \
   python3 $GRAFT_REPO_ROOT/bench.py --cpu-baseline 0 --no-pmc > $GRAFT_REPO_ROOT/gpurun_out/final_prof.log 2>&1
+# batch-32 decode kernel mix (bloom-1b1, prompt 128)
+cd $GRAFT_REPO_ROOT && bash tools/gpu_b32_prof.sh || exit 1
