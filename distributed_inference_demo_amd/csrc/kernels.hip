@@ -1603,7 +1603,7 @@ __device__ unsigned long long g_gemm3_stamps[4096 * 4];
 __host__ __device__ __forceinline__ long gemm3_first(int bb, long T, int G) { return (long)bb * T / G; }
 __host__ __device__ __forceinline__ int gemm3_owner(long x, long T, int G) { return (int)(((x + 1) * G + T - 1) / T - 1); }
 
-template <int EK, int PS>
+template <int EK>
 __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                                          int M, int N, int K, Epi ep) {
   constexpr int BM = 128, BN = 128, BK = 64;
@@ -1858,12 +1858,11 @@ static int gemm3_grid(int M, int N, int K, const Epi& ep) {
   return (int)G;
 }
 
-template <int PS = 2>
 static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int G) {
   switch (ep.kind) {
-    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, PS><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
-    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, PS><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
-    default: gemm_mfma3_kernel<EPI_GELU, PS><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    default: gemm_mfma3_kernel<EPI_GELU><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
   }
 }
 
@@ -2112,7 +2111,7 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
     // 128x128 when it still gives every CU a block (>= 240 blocks), else 64x64, else 64x32
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
     if (const int g3 = gemm3_grid(M, N, K, ep)) {
-      gemm3_launch<2>(x, w, M, N, K, ep, s, g3);
+      gemm3_launch(x, w, M, N, K, ep, s, g3);
     } else if (blocks(128, 128) >= 240) {
       gemm2_launch<128, 128, 1>(x, w, M, N, K, ep, s);
     } else if (blocks(64, 64) >= 128) {

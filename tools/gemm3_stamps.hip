@@ -42,7 +42,7 @@ int main() {
     ep.sk_ws = ws; ep.sk_tickets = tick; ep.sk_cap = cap; ep.sk_ntickets = 4096;
     std::vector<double> ev, span, ramp, pro, loop, epi;
     for (int it = 0; it < 15; it++) {
-      CK(hipEventRecord(e0)); gemm3_launch<2>(X, W, sh.M, sh.N, sh.K, ep, 0, sh.G); CK(hipEventRecord(e1));
+      CK(hipEventRecord(e0)); gemm3_launch(X, W, sh.M, sh.N, sh.K, ep, 0, sh.G); CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_gemm3_stamps), st.size() * 8));

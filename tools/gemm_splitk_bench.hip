@@ -76,7 +76,7 @@ int main() {
     for (int G : {128, 192, 256, 384, 512}) {
       char nm[64];
       snprintf(nm, sizeof nm, "m32 stream-K G=%d", G);
-      const float us = timeit([&] { gemm3_launch<2>(X, W, M, N, K, ep, 0, G); });
+      const float us = timeit([&] { gemm3_launch(X, W, M, N, K, ep, 0, G); });
       CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
       double md = 0;
       for (size_t i = 0; i < ho.size(); i++) md = std::max(md, (double)fabsf(ho[i] - hr[i]));
