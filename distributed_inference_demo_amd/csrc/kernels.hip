@@ -2462,21 +2462,24 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   // one register stage: tile k0 + KT is in flight while tile k0 computes (a second stage, tile k0 + 2 KT,
   // measured no faster: profiles/r03_attn_prefill_split.txt)
   bf16x8 kreg[CPT], vreg[4];
-  auto gload = [&](int k0) {  // clamped: loads past the block's keys re-read its last key
+  auto gload = [&](int k0, int lim) {  // clamped to key lim: loads past it re-read that key
 #pragma unroll
     for (int i = 0; i < CPT; i++) {
       const int c = min(tid + i * 256, nch - 1);
       const int kr = c / nchunk, dc = (c - kr * nchunk) * 8;
-      const int key = min(k0 + kr, kend - 1);
+      const int key = min(k0 + kr, lim);
       kreg[i] = *reinterpret_cast<const bf16x8*>(kb + (size_t)key * hd + dc);
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const int key = min(k0 + vq * 4 + i, kend - 1);
+      const int key = min(k0 + vq * 4 + i, lim);
       vreg[i] = *reinterpret_cast<const bf16x8*>(vb + (size_t)key * hd + vdc);
     }
   };
-  if (kbeg < kstop) gload(kbeg);
+  // The first tile is requested at the split's nominal start, clamped to the cache rather than to the
+  // context, so it does not wait for past_len: keys past the context are masked (p = 0) and the cache
+  // is zero-initialised and only ever holds finite values (0 * V stays 0).  An empty split drops it.
+  gload(nspl > 1 ? min(spl * a.pf_tiles * KT, a.max_ctx - 1) : 0, a.max_ctx - 1);
   for (int k0 = kbeg; k0 < kstop; k0 += KT) {
     __syncthreads();  // previous tile's LDS reads are done
 #pragma unroll
@@ -2497,7 +2500,7 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       }
     }
     __syncthreads();
-    if (k0 + KT < kstop) gload(k0 + KT);  // next tile in flight while this one computes
+    if (k0 + KT < kstop) gload(k0 + KT, kend - 1);  // next tile in flight while this one computes
     // S tiles: four 16-key tiles
     f32x4 sacc[4];
 #pragma unroll
