@@ -1603,13 +1603,12 @@ __device__ unsigned long long g_gemm3_stamps[4096 * 4];
 __host__ __device__ __forceinline__ long gemm3_first(int bb, long T, int G) { return (long)bb * T / G; }
 __host__ __device__ __forceinline__ int gemm3_owner(long x, long T, int G) { return (int)(((x + 1) * G + T - 1) / T - 1); }
 
-template <int EK>
+template <int EK, int NSTG = 3>  // NSTG LDS stages: 3 (96 KB, one block per CU) or 2 (64 KB, two per CU)
 __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                                          int M, int N, int K, Epi ep) {
   constexpr int BM = 128, BN = 128, BK = 64;
   constexpr int NTH = 512;                       // 8 waves: 2 per SIMD, one's MFMAs cover the other's LDS waits
   constexpr int CA = BM * BK / 8 / NTH, CB = BN * BK / 8 / NTH;  // 16-B chunks per thread per stage: 2, 2
-  constexpr int NSTG = 3;                        // LDS stages: tile kt computes while kt + 1, kt + 2 land
   __shared__ __attribute__((aligned(16))) bf16 smem[NSTG * (BM + BN) * BK];  // 96 KB, the only LDS object
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3, r = lane & 31, h = lane >> 5;  // wave tile 64 x 32 at (64 wm, 32 wn)
@@ -1689,17 +1688,17 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
     // __syncthreads() would also wait vmcnt(0) and drain the DMA in flight (cdna_hip_programming.md §5,
     // "Pipelining across barriers").  The previous segment's epilogue ended with a barrier: the LDS is free.
     gload(0, 0);
-    gload(1, 1);
+    if constexpr (NSTG == 3) gload(1, 1);
 #ifdef GEMM3_STAMPS
     if (first_seg) st1 = __builtin_amdgcn_s_memrealtime();
 #endif
-    int buf = 0, nbuf = 2;  // stage of tile kt, stage for tile kt + 2
+    int buf = 0, nbuf = NSTG - 1;  // stage of tile kt, stage for tile kt + NSTG - 1
     for (int kt = 0; kt < kn; kt++) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CA + CB) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTG - 2) * (CA + CB)) : "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      gload(nbuf, kt + 2);
+      gload(nbuf, kt + NSTG - 1);
       ktile(buf);
       buf = buf == NSTG - 1 ? 0 : buf + 1;
       nbuf = nbuf == NSTG - 1 ? 0 : nbuf + 1;
@@ -1858,11 +1857,12 @@ static int gemm3_grid(int M, int N, int K, const Epi& ep) {
   return (int)G;
 }
 
+template <int NSTG = 3>
 static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int G) {
   switch (ep.kind) {
-    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
-    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
-    default: gemm_mfma3_kernel<EPI_GELU><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, NSTG><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, NSTG><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    default: gemm_mfma3_kernel<EPI_GELU, NSTG><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
   }
 }
 

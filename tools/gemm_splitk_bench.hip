@@ -73,10 +73,15 @@ int main() {
     };
     for (int ks : {1, 4})
       variant("64x64 r4", 64, 64, ks, [&] { gemm2_launch<64, 64, 4>(X, W, M, N, K, ep, 0, ks); });
-    for (int G : {128, 192, 256, 384, 512}) {
+    for (int v = 0; v < 6; v++) {
+      const int G = v < 3 ? (int[]){192, 256, 384}[v] : (int[]){256, 384, 512}[v - 3];
+      const int nst = v < 3 ? 3 : 2;
       char nm[64];
-      snprintf(nm, sizeof nm, "m32 stream-K G=%d", G);
-      const float us = timeit([&] { gemm3_launch(X, W, M, N, K, ep, 0, G); });
+      snprintf(nm, sizeof nm, "m32 %dstg G=%d", nst, G);
+      const float us = timeit([&] {
+        if (nst == 3) gemm3_launch<3>(X, W, M, N, K, ep, 0, G);
+        else gemm3_launch<2>(X, W, M, N, K, ep, 0, G);
+      });
       CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
       double md = 0;
       for (size_t i = 0; i < ho.size(); i++) md = std::max(md, (double)fabsf(ho[i] - hr[i]));
