@@ -3,9 +3,10 @@
 N=1 (default): BASELINE.json configs[1] — bloom-1b1 as one stage on one GPU, batch 1,
 512-token prefill (timed separately, reported under "prefill"), then W untimed and K timed
 decode steps.  One "step" = one decode token for every row of the batch through the whole
-model.  N>1 (torchrun, one rank per GPU): the same model split into N stages by the server's
-round-robin layer assignment (server.py:893-905), activations over RCCL send/recv, N rows in
-flight (one per stage) — see distributed_inference_demo_amd/pipeline.py.
+model.  N>1 (one rank per GPU: under torchrun, or `bench.py --gpus N` starts the N ranks
+itself): the same model split into N stages by the server's round-robin layer assignment
+(server.py:893-905), activations over RCCL send/recv, 2N micro-batches in flight, plus the
+configs[3] / configs[4] records — see distributed_inference_demo_amd/pipeline_bench.py.
 
 Prints ONE JSON line (rank 0).  Inputs are resident in HBM before the timed region.
 """
@@ -22,7 +23,7 @@ HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E vendor peak (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA vendor peak
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=128)
@@ -46,7 +47,19 @@ def parse():
     p.add_argument("--no-pipeline-n1", action="store_true",
                    help="N = 1: skip the pipeline code's N = 1 point (the reference point of the N > 1 curve)")
     p.add_argument("--no-strong", action="store_true", help="pipeline: skip the fixed-rows (strong) measurement")
-    return p.parse_args()
+    p.add_argument("--no-configs", action="store_true",
+                   help="pipeline: skip the BASELINE.json configs[3] / configs[4] records")
+    p.add_argument("--configs-model", default="bloom-7b1", help="pipeline: model of the configs[3] / [4] records")
+    p.add_argument("--configs3-mb", type=int, default=8, help="configs[3]: micro-batches of one row (B)")
+    p.add_argument("--configs3-prompt", type=int, default=512, help="configs[3]: prefill tokens per row")
+    p.add_argument("--configs4-rows", type=int, default=32, help="configs[4]: decode batch B")
+    p.add_argument("--configs4-ctx", default="256,512,1024,2048", help="configs[4]: contexts reported")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="pipeline process-group backend (gloo: host tensors, needs --executor)")
+    p.add_argument("--executor", default=None,
+                   help="pipeline: module:function returning the per-stage executor factory for (model, dtype, "
+                        "seed) -- a test hook for the gloo backend (tests/bench_checker.py)")
+    return p.parse_args(argv)
 
 
 def pmc_traffic(args, kernel_tag, timeout=240):
@@ -359,46 +372,65 @@ def _prompt(B, P, V):
     return prompt_ids(1234, B, P, V)
 
 
-def _pipeline_n1(args):
-    """The pipeline code (pipeline.bench_pipeline) at N = 1 on an nccl world-1 group: the point the driver's
-    N > 1 lines (the same code under torchrun) scale from."""
+def _free_port():
     import socket
-    from distributed_inference_demo_amd.pipeline import bench_pipeline
-    if "MASTER_PORT" not in os.environ:
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        os.environ["MASTER_PORT"] = str(s.getsockname()[1])
-        s.close()
-    os.environ.setdefault("RANK", "0")
-    os.environ.setdefault("WORLD_SIZE", "1")
-    os.environ.setdefault("LOCAL_RANK", "0")
-    return bench_pipeline(args)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
-def main():
-    args = parse()
+def _pipeline(args):
+    """pipeline_bench.bench_pipeline on this process's rank (torchrun env, or a world-1 group at N = 1: the
+    point the N > 1 lines -- the same code -- scale from)."""
+    from distributed_inference_demo_amd.pipeline_bench import bench_pipeline
+    if "WORLD_SIZE" not in os.environ:
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    factory = None
+    if args.executor:
+        import importlib
+        mod, fn = args.executor.split(":")
+        factory = getattr(importlib.import_module(mod), fn)
+    return bench_pipeline(args, backend=args.backend, executor_factory=factory)
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` run plainly (no torchrun env): start N rank processes of this same script under
+    torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) and return their exit status.  The parent
+    touches no GPU -- it only waits -- and rank 0's JSON line reaches stdout through the shared descriptor;
+    torchrun stops every rank and exits non-zero if any rank fails."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} started with WORLD_SIZE={world}")
     # the driver reads ONE JSON line from stdout: libraries that print banners there (RCCL prints its version
     # block when a communicator is created) are sent to stderr at the file-descriptor level
     out_fd = os.dup(1)
     sys.stdout.flush()
     os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     ranges = model = None
-    if world > 1 or args.gpus > 1 or args.pipeline:
-        if world == 1:
-            res, ranges, model = _pipeline_n1(args)
-        else:
-            from distributed_inference_demo_amd.pipeline import bench_pipeline
-            res, ranges, model = bench_pipeline(args)
+    if world > 1 or args.pipeline:
+        res, ranges, model = _pipeline(args)
     else:
         res = bench_single(args)
         if not args.no_pipeline_n1:
-            p1, _, _ = _pipeline_n1(args)
+            p1, _, _ = _pipeline(args)
             res["pipeline_n1"] = {k: p1[k] for k in ("value", "ms_per_step", "config", "weak_definition", "stage_hbm",
-                                                     "prefill") if k in p1}
-            if "strong" in p1:
-                res["pipeline_n1"]["strong"] = p1["strong"]
-            res["pipeline_n1"]["note"] = ("pipeline.bench_pipeline at N = 1 (nccl world-1 group, StageExecutor, "
+                                                     "prefill", "strong", "configs3", "configs4") if k in p1}
+            res["pipeline_n1"]["note"] = ("pipeline_bench.bench_pipeline at N = 1 (nccl world-1 group, StageExecutor, "
                                           "graph-replayed decode): the same code and definitions as the N > 1 lines")
         from distributed_inference_demo_amd import config
         model = config.get(args.model)
@@ -407,7 +439,8 @@ def main():
     sys.stdout.flush()
     if res is not None:
         os.write(out_fd, (json.dumps(res) + "\n").encode())
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

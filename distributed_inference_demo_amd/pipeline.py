@@ -146,6 +146,11 @@ class Pipeline:
         if timing is None:
             self.ex.forward(inp, out, self.mb, seq, slot, self.past[j])
             return
+        if self.dev.type != "cuda":  # host executors run synchronously: host-clock pairs in ms
+            t0 = time.perf_counter() * 1e3
+            self.ex.forward(inp, out, self.mb, seq, slot, self.past[j])
+            timing.append((t0, time.perf_counter() * 1e3))
+            return
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         self.ex.forward(inp, out, self.mb, seq, slot, self.past[j])
@@ -159,8 +164,9 @@ class Pipeline:
         Continuous batching (serve.py): `pasts[j]` = every row's own position this round (all
         ranks, the same schedule); `feed[j]` = (tokens, mask) int32/bool [mb] on rank 0's device:
         rows with mask set take `tokens` (a prompt token, or a new sample's first token) instead of
-        the token the pipeline returned for them.  `timing` (a list, CUDA ranks): one event pair per
-        stage forward of this round is appended (stage busy time, bench_pipeline's prefill overlap)."""
+        the token the pipeline returned for them.  `timing` (a list): one (start, end) pair per stage
+        forward of this round is appended -- HIP events on CUDA ranks, host-clock ms otherwise (stage
+        busy time, pipeline_bench's prefill overlap)."""
         n_el = self.mb * seq * self.h
         for j in range(self.n_mb):
             slot = j * self.mb
@@ -330,175 +336,3 @@ def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb
                     is_first=is_first, is_last=is_last, tok_group=tok_group, head_group=head_group,
                     head_split=head_split, act_dtype=act, max_seq=max_seq)
     return pipe, (lb, le)
-
-
-def _stage_step_bytes(model, lb, le, rows, ctx, first, last, hslice, w_bytes, kv_bytes):
-    """Algorithmic HBM bytes of one decode forward of a stage (BASELINE.md formula) plus, with the
-    vocabulary-parallel head, the stage's lm_head slice and ln_f."""
-    b = config.decode_step_bytes(model, le - lb, rows, ctx, first, last, w_bytes=w_bytes, kv_bytes=kv_bytes)
-    if hslice is not None:
-        b += (hslice[1] - hslice[0]) * model.hidden * w_bytes + 2 * model.hidden * w_bytes
-    return b
-
-
-def _max_over_ranks(x, dev):
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def run_pipeline(args, model, rank, world, dev, *, mb_rows, n_mb, head_split, prof_rounds):
-    """One pipeline measurement: a timed P-token prefill round (with per-stage forward events), W warm-up
-    and K timed decode rounds (barrier + sync on both sides, max over ranks), then `prof_rounds` eager
-    rounds with HIP events around every decode weight GEMV.  Collective; rank 0 returns the dict."""
-    B, P, K, W = mb_rows, args.prompt, args.steps, args.warmup
-    pipe, (lb, le) = build_rank(model, rank, world, dev, dtype=args.dtype, mb_rows=B, n_mb=n_mb,
-                                max_ctx=P + W + K + prof_rounds + 2, max_seq=P, seed=args.seed, head_split=head_split)
-    cs = torch.cuda.Stream()  # a real stream: decode steps are captured as hipGraphs
-    prev = torch.cuda.current_stream()
-    torch.cuda.set_stream(cs)
-    prompt = None
-    if rank == 0:
-        from .stage import prompt_ids
-        prompt = torch.from_numpy(prompt_ids(1234, B * n_mb, P, model.vocab)).to(dev)
-    dist.barrier()
-    torch.cuda.synchronize()
-    # prefill round (the micro-batches stream through the stages: configs[3]'s overlap)
-    timing = []
-    t0 = time.perf_counter()
-    pipe.step(P, prompt=prompt, timing=timing)
-    torch.cuda.synchronize()
-    t_pre = time.perf_counter() - t0
-    busy_ms = sum(a.elapsed_time(b) for a, b in timing)
-    t_pre = _max_over_ranks(t_pre, dev)
-    for _ in range(W):
-        pipe.step(1)
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(K):
-        pipe.step(1)
-    pipe.finish()
-    torch.cuda.synchronize()
-    dist.barrier()
-    dt = _max_over_ranks(time.perf_counter() - t0, dev)
-    t_round = dt / K
-    # per-stage roofline: eager rounds with HIP events around every decode weight GEMV of this stage
-    st = pipe.ex.stage if hasattr(pipe.ex, "stage") else None
-    g = None
-    if st is not None and prof_rounds:
-        st.profile_enable(1)
-        for _ in range(prof_rounds):
-            pipe.step(1)
-        pipe.finish()
-        torch.cuda.synchronize()
-        g = st.profile_read()
-        st.profile_enable(0)
-    dist.barrier()
-    hslice = vocab_slices(model.vocab, world)[rank] if pipe.head_split else None
-    w_b = 2 if args.dtype == "bf16" else 4
-    ctx_mid = P + W + K / 2
-    step_bytes = _stage_step_bytes(model, lb, le, B, ctx_mid, rank == 0, rank == world - 1 and not pipe.head_split,
-                                   hslice, w_b, w_b)
-    if model.int8_weights:
-        step_bytes -= (le - lb) * (12.0 * model.hidden * model.hidden * 1 - 9.0 * model.hidden * 4)
-    pre_flops = config.prefill_flops(model, le - lb, B * n_mb, P, False)
-    mine = {"rank": rank, "layers": [lb, le], "head_slice": list(hslice) if hslice else None,
-            "algo_bytes_per_forward": step_bytes,
-            "achieved_GBps": n_mb * step_bytes / t_round / 1e9,
-            "prefill": {"busy_ms": busy_ms, "busy_frac": busy_ms / (t_pre * 1e3),
-                        "stage_TFLOPs": pre_flops / (busy_ms * 1e-3) / 1e12 if busy_ms > 0 else None}}
-    mine["frac_of_peak"] = mine["achieved_GBps"] / 8000.0
-    if g is not None and g[1]:
-        ms, n, byts = g
-        mine["gemv"] = {"launches": n, "avg_us": ms / n * 1e3, "achieved_GBps": (byts / n) / (ms / n * 1e-3) / 1e9}
-    allst = [None] * world
-    dist.all_gather_object(allst, mine)
-    torch.cuda.set_stream(prev)
-    st_close = getattr(st, "close", None)
-    del pipe
-    if st_close:
-        st_close()
-    if rank != 0:
-        return None
-    toks = B * n_mb * K
-    res = {"value": toks / dt, "ms_per_step": dt * 1e3 / K, "rows": B * n_mb, "micro_batch": B, "n_mb": n_mb,
-           "head": "vocab-split ring" if head_split and world > 1 else "last stage", "per_stage": allst,
-           "stage_hbm": {"achieved_GBps_min": min(x["achieved_GBps"] for x in allst),
-                         "achieved_GBps_mean": sum(x["achieved_GBps"] for x in allst) / world,
-                         "frac_of_peak_min": min(x["frac_of_peak"] for x in allst),
-                         "frac_of_peak_mean": sum(x["frac_of_peak"] for x in allst) / world,
-                         "note": "per stage: n_mb x algorithmic bytes of one forward / time of one pipeline round"}}
-    tot_flops = config.prefill_flops(model, model.n_layer, B * n_mb, P, True)
-    res["prefill"] = {"tokens": B * n_mb * P, "ms": t_pre * 1e3, "tokens_per_s": B * n_mb * P / t_pre,
-                      "achieved_TFLOPs": tot_flops / t_pre / 1e12,
-                      "frac_of_peak": tot_flops / t_pre / 1e12 / 2500.0,
-                      "stage_busy_frac": [x["prefill"]["busy_frac"] for x in allst],
-                      "ideal_busy_frac": n_mb / (n_mb + world - 1),
-                      "note": "busy = sum of a stage's forward times (HIP events) / prefill round wall time; "
-                              "ideal = n_mb / (n_mb + stages - 1) for a perfectly overlapped fill-and-drain"}
-    gemv = [x["gemv"] for x in allst if "gemv" in x]
-    if gemv:
-        tot_t = sum(x["launches"] * x["avg_us"] for x in gemv)
-        tot_b = sum(x["launches"] * x["avg_us"] * 1e-6 * x["achieved_GBps"] * 1e9 for x in gemv)
-        ach = tot_b / (tot_t * 1e-6) / 1e9
-        res["roofline"] = {"bound": "hbm", "kernel": "decode weight GEMVs of every stage (gemv_rows_kernel, "
-                                                     "gemv_ldsw4_kernel)",
-                           "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0, "traffic": None,
-                           "traffic_note": "PMC passes need one rocprofv3 process per rank; collected at N = 1 only",
-                           "launches": sum(x["launches"] for x in gemv),
-                           "avg_us": tot_t / sum(x["launches"] for x in gemv),
-                           "measured": f"HIP events per launch on each stage's stream, {prof_rounds} eager pipeline "
-                                       "rounds after the timed region; bytes and time summed over all stages"}
-    return res
-
-
-def bench_pipeline(args):
-    """bench.py under torchrun (or --pipeline at N = 1): the model split into N stages, measured twice with
-    the same code -- "weak": 2N micro-batches of `batch` rows (every GPU runs 2 x n_layer / N x N = 2 x
-    n_layer layer-forwards of `batch` rows per round at every N, so per-GPU work is fixed), the line's
-    `value`; "strong": 16 x `batch` rows at every N (2N micro-batches of 8 x batch / N rows).
-    Rank 0 returns (line dict, stage ranges, model) -- the ranges for the host-CPU baseline of the split."""
-    rank, world, local = init_distributed("nccl")
-    dev = torch.device("cuda", local)
-    model = config.get(args.model)
-    if getattr(args, "weights", "bf16") == "int8":
-        model = config.get(model.name if model.int8_weights else model.name + "-int8")
-    prof_rounds = 0 if getattr(args, "no_profile", False) else 8
-    head_split = not getattr(args, "no_head_split", False)
-    n_mb = 2 * world
-    weak = run_pipeline(args, model, rank, world, dev, mb_rows=args.batch, n_mb=n_mb, head_split=head_split,
-                        prof_rounds=prof_rounds)
-    strong = None
-    if not getattr(args, "no_strong", False):
-        rows = 16 * args.batch
-        strong = run_pipeline(args, model, rank, world, dev, mb_rows=max(1, rows // n_mb), n_mb=n_mb,
-                              head_split=head_split, prof_rounds=0)
-    dist.barrier()
-    dist.destroy_process_group()
-    if rank != 0:
-        return None, stage_ranges(world, model.n_layer), model
-    per_stage = [b - a for a, b in stage_ranges(world, model.n_layer)]
-    res = {
-        "metric": "decode tokens/s, BLOOM pipeline", "value": weak["value"], "unit": "tokens/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": weak["ms_per_step"], "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-        "data": "synthetic: repo-generator random-init weights (seed %d), prompt ids U[0,V) seed 1234" % args.seed,
-        "config": {"workload": f"{model.name} split into {world} stages by the server's round-robin layer "
-                               f"assignment, {n_mb} micro-batches x {args.batch} rows in flight, RCCL send/recv"
-                               + (", vocabulary-parallel lm_head ring" if weak["head"] == "vocab-split ring" else ""),
-                   "model": model.name, "stages": world, "layers_per_stage": per_stage, "batch": weak["rows"],
-                   "micro_batch": args.batch, "prompt": args.prompt, "parallelism": f"pp{world}",
-                   "head": weak["head"],
-                   "hop": "fp32 hidden [mb, S, h] (the reference wire dtype; keeps the split bit-identical to one stage)"},
-        "weak_definition": "2N micro-batches x batch rows: per-GPU layer-forwards per round fixed at 2 x n_layer",
-        "per_stage": weak["per_stage"], "stage_hbm": weak["stage_hbm"], "prefill": weak["prefill"],
-    }
-    if "roofline" in weak:
-        res["roofline"] = weak["roofline"]
-    if strong is not None:
-        res["strong"] = {k: strong[k] for k in ("value", "ms_per_step", "rows", "micro_batch", "n_mb", "stage_hbm",
-                                                "prefill")}
-        res["strong"]["definition"] = "16 x batch rows in flight at every N (2N micro-batches of 8 x batch / N rows)"
-    return res, stage_ranges(world, model.n_layer), model

@@ -98,7 +98,7 @@ def _run(world, head_split, resume, model=MODEL):
         p.start()
     got, ranges = None, {}
     while got is None or len(ranges) < world:
-        msg = q.get(timeout=180)
+        msg = q.get(timeout=420)
         if msg[0] == "tokens":
             got = msg[1]
         else:
