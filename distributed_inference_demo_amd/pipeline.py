@@ -77,18 +77,23 @@ class Pipeline:
     With world == 1 the single stage loops its own tokens back (no communication)."""
 
     def __init__(self, executor, *, rank, world, hidden, mb_rows, n_mb, device, is_first, is_last,
-                 tok_group=None, head_group=None, head_split=False, act_dtype=torch.float32, max_seq=1):
+                 tok_group=None, head_group=None, head_split=False, act_dtype=torch.float32, max_seq=1,
+                 pf_group=None):
         self.ex, self.rank, self.world = executor, rank, world
         self.h, self.mb, self.n_mb, self.dev = hidden, mb_rows, n_mb, device
         self.is_first, self.is_last = is_first, is_last
-        self.tok_group, self.head_group = tok_group, head_group
+        self.tok_group, self.head_group, self.pf_group = tok_group, head_group, pf_group
         self.head_split = head_split and world > 1
         f32, i32 = torch.float32, torch.int32
         self.hin = [torch.empty(mb_rows * max_seq * hidden, dtype=f32, device=device) for _ in range(n_mb)]
         self.hout = [torch.empty(mb_rows * max_seq * hidden, dtype=f32, device=device) for _ in range(n_mb)]
         self.tok = [torch.zeros(mb_rows, dtype=i32, device=device) for _ in range(n_mb)]
+        self.pf_tok = [torch.zeros(mb_rows, dtype=i32, device=device) for _ in range(n_mb)]  # prefill_row's tokens
         self.pending = [[] for _ in range(n_mb)]
         self.hpending = [[] for _ in range(n_mb)]
+        # token returns of the decode rounds (tok_group), kept apart: rank 0 receives a round's tokens only at
+        # the start of the next round, so a prefill_row pass in between must not wait for them
+        self.tsend = [[] for _ in range(n_mb)]
         self.past = [0] * n_mb
         self.tokens_held = False  # after finish(): rank 0 already holds every micro-batch's next input
         if self.head_split:
@@ -115,6 +120,7 @@ class Pipeline:
         prev = self.world - 1 if self.rank == 0 else self.rank - 1
         with self._hctx():
             self._drain(self.hpending[j])
+            self._drain(self.tsend[j])
             _recv(self.xn[j], prev, self.head_group)
             _recv(self.kin[j], prev, self.head_group)
             if self.rank == self.closer:
@@ -123,7 +129,7 @@ class Pipeline:
                     if self.tok_ready is not None:
                         self.tok_ready[j].record()
                 else:
-                    self.hpending[j].append(dist.isend(self.tok[j], dst=0, group=self.tok_group))
+                    self.tsend[j].append(dist.isend(self.tok[j], dst=0, group=self.tok_group))
             else:
                 self.ex.head_slice(self.xn[j], self.mb, self.kin[j], self.kout[j], None)
                 self.hpending[j].append(dist.isend(self.xn[j], dst=self.rank + 1, group=self.head_group))
@@ -173,6 +179,8 @@ class Pipeline:
             if pasts is not None:
                 self.past[j] = list(pasts[j])
             self._drain(self.pending[j])
+            if not self.head_split:
+                self._drain(self.tsend[j])
             if self.is_first:
                 if prompt is not None:
                     inp = prompt[j * self.mb:(j + 1) * self.mb].contiguous()
@@ -188,7 +196,7 @@ class Pipeline:
             if self.is_last and not self.head_split:
                 self._forward(inp, self.tok[j], seq, slot, j, timing)
                 if self.world > 1:
-                    self.pending[j].append(dist.isend(self.tok[j], dst=0, group=self.tok_group))
+                    self.tsend[j].append(dist.isend(self.tok[j], dst=0, group=self.tok_group))
                 elif record is not None:
                     record[j].append(self.tok[j].clone())
             else:
@@ -206,6 +214,55 @@ class Pipeline:
             self.past[j] = [p + seq for p in self.past[j]] if isinstance(self.past[j], list) else self.past[j] + seq
         self.tokens_held = False
 
+    def prefill_row(self, j, r, ids, n):
+        """One pipeline pass of row r of micro-batch j alone: its n prompt tokens at positions 0..n-1 of KV slot
+        j * mb + r (a new sample taking the row: serve.py's admission prefill, Communication.java:418-464).
+        `ids` int32 [1, n] on rank 0 (None elsewhere).  The first generated token lands in self.pf_tok[j][r] on
+        rank 0 (stream-ordered); it travels on `pf_group`, so it never interleaves with the decode rounds'
+        token returns on `tok_group`.  Every rank calls this in the same order as every other rank."""
+        n_el, h = n * self.h, self.h
+        slot = j * self.mb + r
+        tok = self.pf_tok[j][r:r + 1]
+        self._drain(self.pending[j])
+        if self.is_first:
+            inp = ids
+        else:
+            inp = self.hin[j][:n_el]
+            _recv(inp, self.rank - 1)
+        if self.is_last and not self.head_split:
+            self.ex.forward(inp, tok, 1, n, slot, 0)
+            if self.world > 1:
+                self.pending[j].append(dist.isend(tok, dst=0, group=self.pf_group))
+        else:
+            out = self.hout[j][:n_el]
+            self.ex.forward(inp, out, 1, n, slot, 0)
+            if not self.is_last:
+                self.pending[j].append(dist.isend(out, dst=self.rank + 1))
+            else:  # head_split: open the head ring
+                self.ex.head_norm(out, 1, n, self.xn[j][:h])
+                self.ex.head_slice(self.xn[j][:h], 1, None, self.kout[j][:1], None)
+                self.pending[j].append(dist.isend(self.xn[j][:h], dst=0, group=self.head_group))
+                self.pending[j].append(dist.isend(self.kout[j][:1], dst=0, group=self.head_group))
+        if self.head_split and self.rank <= self.closer:
+            prev = self.world - 1 if self.rank == 0 else self.rank - 1
+            with self._hctx():
+                self._drain(self.hpending[j])
+                _recv(self.xn[j][:h], prev, self.head_group)
+                _recv(self.kin[j][:1], prev, self.head_group)
+                if self.rank == self.closer:
+                    self.ex.head_slice(self.xn[j][:h], 1, self.kin[j][:1], None, tok)
+                    if self.rank != 0:
+                        self.hpending[j].append(dist.isend(tok, dst=0, group=self.pf_group))
+                else:
+                    self.ex.head_slice(self.xn[j][:h], 1, self.kin[j][:1], self.kout[j][:1], None)
+                    self.hpending[j].append(dist.isend(self.xn[j][:h], dst=self.rank + 1, group=self.head_group))
+                    self.hpending[j].append(dist.isend(self.kout[j][:1], dst=self.rank + 1, group=self.head_group))
+            if self.rank == 0 and self.closer == 0 and self.hstream is not None:
+                torch.cuda.current_stream().wait_stream(self.hstream)
+        if self.is_first and self.world > 1 and not (self.head_split and self.closer == 0):
+            _recv(tok, self.closer if self.head_split else self.world - 1, self.pf_group)
+        return tok
+
     def finish(self, record=None):
         """Rank 0 collects the tokens of the last round; everyone drains its sends.  Later steps
         continue from those tokens."""
@@ -216,6 +273,7 @@ class Pipeline:
         for j in range(self.n_mb):
             self._drain(self.pending[j])
             self._drain(self.hpending[j])
+            self._drain(self.tsend[j])
         if self.head_split and self.hstream is not None:
             torch.cuda.current_stream().wait_stream(self.hstream)
 
@@ -268,7 +326,8 @@ def p2p_edges(world, head_split):
     """Every directed point-to-point edge the schedule uses, as (group name, src, dst), in one global order:
     hidden states r -> r+1 ("hidden"), the head ring N-1 -> 0 -> 1 -> ... -> N-2 ("head", a chain that ends
     at the closer N-2: no edge closes the cycle), tokens back to rank 0 ("tok", from the closer or from the
-    last rank)."""
+    last rank) and the admission prefills' first tokens ("pf", the same two ranks on a communicator of
+    their own)."""
     if world <= 1:
         return []
     e = [("hidden", r, r + 1) for r in range(world - 1)]
@@ -278,8 +337,10 @@ def p2p_edges(world, head_split):
         e += [("head", a, b) for a, b in zip(ring, ring[1:])]
         if closer != 0:
             e.append(("tok", closer, 0))
+            e.append(("pf", closer, 0))
     else:
         e.append(("tok", world - 1, 0))
+        e.append(("pf", world - 1, 0))
     return e
 
 
@@ -326,13 +387,15 @@ def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb
     else:
         ex = executor_factory(lb, le, is_first, is_last and not head_split, mb_rows * n_mb, max_ctx, hslice)
     # communicators are created collectively, in the same order on every rank
-    tok_group = head_group = None
+    tok_group = head_group = pf_group = None
     if world > 1:
         tok_group = dist.new_group(ranks=list(range(world)))
         head_group = dist.new_group(ranks=list(range(world)))
-        connect_p2p(rank, world, head_split, {"hidden": None, "head": head_group, "tok": tok_group}, device)
+        pf_group = dist.new_group(ranks=list(range(world)))
+        connect_p2p(rank, world, head_split, {"hidden": None, "head": head_group, "tok": tok_group, "pf": pf_group},
+                    device)
     act = torch.bfloat16 if dtype == "bf16" else torch.float32
     pipe = Pipeline(ex, rank=rank, world=world, hidden=model.hidden, mb_rows=mb_rows, n_mb=n_mb, device=device,
                     is_first=is_first, is_last=is_last, tok_group=tok_group, head_group=head_group,
-                    head_split=head_split, act_dtype=act, max_seq=max_seq)
+                    head_split=head_split, act_dtype=act, max_seq=max_seq, pf_group=pf_group)
     return pipe, (lb, le)

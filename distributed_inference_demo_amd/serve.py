@@ -15,10 +15,13 @@ placement (`placement.stage_ranges`).  Lifecycle:
            the hops overlap;
   run    — continuous admission (Communication.java:418-464: a new sample starts as soon as one in
            flight finishes): a row takes the next sample the round its previous sample produced its
-           `max_length`-th token.  Rounds are S = 1 for every row: a sample's prompt is fed one token
-           a round (the reference header also feeds single tokens, Communication.java:322-326), then
-           its own greedy tokens.  Prompts may have different lengths.  The admission schedule depends
-           only on the prompt lengths, so every rank derives the same per-row positions;
+           `max_length`-th token.  The admitted sample's whole prompt goes through the stages as one
+           prefill pass of that row (S = len(prompt) at its KV slot, Pipeline.prefill_row) just before
+           the decode round, which it joins with its first generated token; decode rounds are S = 1 for
+           every row, each at its own position.  (prefill=False feeds the prompt one token a round, as
+           the reference header does, Communication.java:322-326.)  Prompts may have different lengths.
+           The admission schedule depends only on the prompt lengths, so every rank derives the same
+           per-row positions and prefill passes;
   finish — rank 0 returns every sample's `max_length` greedy token ids and the run's tokens/s.
 Differences from the reference, by design: full-context decode (the reference
 header feeds only the last token), argmax instead of unseeded top-k, token ids in (no tokenizer).
@@ -54,6 +57,7 @@ class RunConfig:
     dtype: str = "bf16"
     seed: int = 0                 # weight generator seed
     head_split: bool = True       # vocabulary-parallel lm_head ring when world > 1
+    prefill: bool = True          # an admitted sample's prompt as one prefill pass of its row (else a token a round)
 
 
 def synthetic_prompts(cfg: RunConfig, vocab):
@@ -61,20 +65,25 @@ def synthetic_prompts(cfg: RunConfig, vocab):
     return [prompt_ids(1234 + i, 1, cfg.prompt_len, vocab).reshape(-1).tolist() for i in range(cfg.num_sample)]
 
 
-def admission_schedule(lens, max_length, rows):
+def admission_schedule(lens, max_length, rows, prefill=True):
     """Row-level continuous admission: sample i (in order) takes the row that frees first (lowest row
-    on ties) at the round it frees; it occupies the row for len(prompt) - 1 + max_length rounds (its
-    prompt tokens, then max_length generated ones, the last of which is never fed back).
-    Returns ([(row, start_round)] per sample, total rounds)."""
+    on ties) at the round it frees.
+      prefill=True : the sample's whole prompt is one prefill pass of that row just before decode round t0
+                     (Pipeline.prefill_row; it yields generated token 1), then it decodes max_length - 1 rounds
+                     (tokens 2..max_length); the row frees at t0 + max_length - 1.
+      prefill=False: the prompt is fed one token a round (the reference header's single-token feed), so the
+                     row is held len(prompt) - 1 + max_length rounds.
+    Returns ([(row, t0)] per sample, total decode rounds)."""
     import heapq
     free = [(0, r) for r in range(rows)]
     heapq.heapify(free)
     out = []
+    hold = (lambda n: max_length - 1) if prefill else (lambda n: n - 1 + max_length)
     for n in lens:
         t, r = heapq.heappop(free)
         out.append((r, t))
-        heapq.heappush(free, (t + n - 1 + max_length, r))
-    return out, max(t + n - 1 + max_length for (r, t), n in zip(out, lens))
+        heapq.heappush(free, (t + hold(n), r))
+    return out, max(t + hold(n) for (r, t), n in zip(out, lens))
 
 
 def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory=None, log=None):
@@ -105,54 +114,85 @@ def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory
     n_mb = min(cfg.core_pool_size, world)
     mb = -(-cfg.core_pool_size // n_mb)
     rows = n_mb * mb
-    sched, T = admission_schedule(lens, cfg.max_length, rows)
-    # per round and row: position, and (rank 0) the fed token / whether it overrides the returned one
+    pf = cfg.prefill
+    sched, T = admission_schedule(lens, cfg.max_length, rows, prefill=pf)
+    # per decode round and row: position, and (rank 0) the fed token / whether it overrides the returned one;
+    # with prefill, `take_pf` marks a sample's first decode round, whose input is its prefill's token
     pos = [[0] * rows for _ in range(T)]
     feed_tok = [[0] * rows for _ in range(T)]
     feed_mask = [[True] * rows for _ in range(T)]
+    take_pf = [[False] * rows for _ in range(T)]
+    admit = [[] for _ in range(T + 1)]  # prefill passes before decode round t: (sample, row)
     for i, ((r, t0), n) in enumerate(zip(sched, lens)):
-        for t in range(t0, t0 + n - 1 + cfg.max_length):
-            pos[t][r] = t - t0
-            if t - t0 < n:
-                feed_tok[t][r] = prompts[i][t - t0] if rank == 0 else 0
-            else:
-                feed_mask[t][r] = False
+        if pf:
+            admit[t0].append((i, r))
+            for t in range(t0, t0 + cfg.max_length - 1):
+                pos[t][r] = n + (t - t0)
+                feed_mask[t][r] = t == t0
+                take_pf[t][r] = t == t0
+        else:
+            for t in range(t0, t0 + n - 1 + cfg.max_length):
+                pos[t][r] = t - t0
+                if t - t0 < n:
+                    feed_tok[t][r] = prompts[i][t - t0] if rank == 0 else 0
+                else:
+                    feed_mask[t][r] = False
     # ---- init (Ready)
+    max_seq = -(-max(lens) // mb) if pf else 1  # a prefill pass of one row fits a micro-batch's hop buffers
     pipe, (lb, le) = build_rank(model, rank, world, device, dtype=cfg.dtype, mb_rows=mb, n_mb=n_mb,
-                                max_ctx=max(lens) + cfg.max_length + 1, max_seq=1, seed=cfg.seed,
+                                max_ctx=max(lens) + cfg.max_length + 1, max_seq=max_seq, seed=cfg.seed,
                                 head_split=cfg.head_split, executor_factory=executor_factory)
     say(STATES[0], {"rank_layers": [lb, le], "stages": world, "core_pool_size": cfg.core_pool_size,
-                    "micro_batches": n_mb, "rows_per_micro_batch": mb, "rounds": T})
+                    "micro_batches": n_mb, "rows_per_micro_batch": mb, "rounds": T, "prefill": pf})
     cuda = device.type == "cuda"
     if cuda:
         torch.cuda.set_stream(torch.cuda.Stream(device))  # decode steps are captured as hipGraphs
-    ft = torch.tensor(feed_tok, dtype=torch.int32, device=device).view(T, n_mb, mb)
-    fm = torch.tensor(feed_mask, dtype=torch.bool, device=device).view(T, n_mb, mb)
+    shape = (max(T, 1), n_mb, mb)
+    ft = torch.tensor(feed_tok or [[0] * rows], dtype=torch.int32, device=device).view(shape)
+    fm = torch.tensor(feed_mask or [[True] * rows], dtype=torch.bool, device=device).view(shape)
+    tp = torch.tensor(take_pf or [[False] * rows], dtype=torch.bool, device=device).view(shape)
+    pids = ([torch.tensor(p, dtype=torch.int32, device=device).view(1, -1) for p in prompts]
+            if (pf and rank == 0) else None)
     if world > 1:
         dist.barrier()
     # ---- run (Running)
     say(STATES[1], {"num_sample": cfg.num_sample, "max_length": cfg.max_length})
     rec = [[] for _ in range(n_mb)] if pipe.is_first else None
+    first = [None] * cfg.num_sample  # prefill: each sample's first generated token (rank 0)
     pipe.tokens_held = True  # round 0 feeds every row
-    t0 = time.perf_counter()
-    for t in range(T):
+    t_start = time.perf_counter()
+    for t in range(T + 1):
+        for i, r in admit[t] if pf else ():
+            tok = pipe.prefill_row(r // mb, r % mb, pids[i] if pids is not None else None, lens[i])
+            if rank == 0:
+                first[i] = tok.clone()
+        if t == T:
+            break
         pasts = [pos[t][j * mb:(j + 1) * mb] for j in range(n_mb)]
-        feed = [(ft[t, j], fm[t, j]) for j in range(n_mb)] if pipe.is_first else None
+        feed = None
+        if pipe.is_first:
+            feed = [((torch.where(tp[t, j], pipe.pf_tok[j], ft[t, j]) if pf else ft[t, j]), fm[t, j])
+                    for j in range(n_mb)]
         pipe.step(1, record=rec, feed=feed, pasts=pasts)
-    pipe.finish(record=rec)
+    if T:
+        pipe.finish(record=rec)
     if cuda:
         torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt = time.perf_counter() - t_start
     # ---- finish (Finish, Close)
     if world > 1:
         dist.barrier()
     if rank != 0:
         return None
-    y = torch.stack([torch.stack(r, 0) for r in rec], 1).view(T, rows).cpu()  # returned token of round t
-    out = [y[t0 + n - 1:t0 + n - 1 + cfg.max_length, r].tolist() for (r, t0), n in zip(sched, lens)]
+    y = torch.stack([torch.stack(r, 0) for r in rec], 1).view(T, rows).cpu() if T else None  # round t's tokens
+    if pf:
+        out = [[int(first[i].item())] + (y[t0:t0 + cfg.max_length - 1, r].tolist() if T else [])
+               for i, (r, t0) in enumerate(sched)]
+    else:
+        out = [y[t0 + n - 1:t0 + n - 1 + cfg.max_length, r].tolist() for (r, t0), n in zip(sched, lens)]
     res = {"samples": out, "num_sample": cfg.num_sample, "max_length": cfg.max_length,
            "core_pool_size": cfg.core_pool_size, "stages": world, "prompt_lens": lens, "rounds": T,
-           "seconds": dt, "tokens_per_s": cfg.num_sample * cfg.max_length / dt}
+           "prefill": pf, "seconds": dt, "tokens_per_s": cfg.num_sample * cfg.max_length / dt}
     say(STATES[2], {k: v for k, v in res.items() if k != "samples"})
     say(STATES[3], {})
     return res

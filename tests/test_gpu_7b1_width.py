@@ -12,9 +12,9 @@ The checker (oracle/bloom_oracle.c, bf16 mode) cannot afford 2000 decode steps o
 so between checkpoints the device runs free (its own argmax tokens) and at each checkpoint the device
 cache written since the last one is handed to the checker (bs_read_kv -> or_write_kv); then both run the
 checkpoint step from the same token: ids equal unless the checker's top-2 margin is < 2e-2, logits within
-the wide-width bound (max-abs <= 2.5e-2, mean-abs <= 4e-3: the rule test_gpu_full_size.py states for full
-depth -- at h = 4096 one rounding flip of an intermediate moves a logit 1.6x as far as at h = 1536, and the
-first device run measured 0.0216 max at the prefill, the same bf16 flip noise), and the K/V rows the step
+north_star's 2e-2 max-abs (mean-abs <= 4e-3) of the checker run with float64 dot-product accumulation (the
+same bf16 storage points; round 3 measured 0.0216 against the fp32-accumulating checker, whose own distance
+to the float64 one is now recorded beside every check), and the K/V rows the step
 appends (the device's QKV epilogue vs the checker's projection) within the wide-block hidden-state bound plus
 one bf16 storage ulp (check_bf16_stored: cached values are rounded to bf16, and two correct paths may round a
 value in [4, 8) to neighbours 0.03125 apart).  The prompt's cache is the checker's own and is
@@ -32,15 +32,34 @@ from distributed_inference_demo_amd.stage import Stage
 from oracle import gen_np
 from oracle.oracle import OracleStage
 
-from test_gpu_parity import assert_ids_match, check_bf16_stored, check_close
+from oracle.oracle import lib as oracle_lib
+from test_gpu_parity import BF16_TOL, assert_ids_match, check_bf16_stored, check_close, record_error
 
-WIDE_LOGIT_TOL, WIDE_LOGIT_MEAN_TOL = 2.5e-2, 4e-3
+WIDE_LOGIT_MEAN_TOL = 4e-3
 
 
-def check_logits_wide(got, ref, what):
-    err, mean = float(np.abs(got - ref).max()), float(np.abs(got - ref).mean())
-    assert err <= WIDE_LOGIT_TOL and mean <= WIDE_LOGIT_MEAN_TOL, f"{what}: logits max-abs {err}, mean-abs {mean}"
+def check_logits_wide(got, ref32, ref64, what):
+    """Logits at h = 4096: north_star's flat 2e-2 max-abs (and mean-abs <= 4e-3) against the checker with
+    float64 dot-product accumulation (or_set_accum_double; the same bf16 storage points).  The fp32 checker
+    is itself one fp32 summation order among many: its distance to the float64 one and the device's distance
+    to it are recorded beside the bound (gpurun_out/parity_errors.jsonl -> profiles/), so the margin and the
+    checker's own noise at this width are on record."""
+    record_error(f"{what} [fp32 checker vs float64 checker]", ref32, ref64, 0.0, "checker noise")
+    record_error(f"{what} [device vs fp32 checker]", got, ref32, 0.0, "logits bf16 (recorded)")
+    err = record_error(what, got, ref64, BF16_TOL, "logits bf16 vs float64 checker")
+    mean = float(np.abs(got - ref64).mean())
+    assert err <= BF16_TOL and mean <= WIDE_LOGIT_MEAN_TOL, f"{what}: logits max-abs {err}, mean-abs {mean}"
     return err
+
+
+class _Accum64:
+    """The checker's float64 accumulation for the calls inside the block (a global knob of liboracle)."""
+
+    def __enter__(self):
+        oracle_lib().or_set_accum_double(1)
+
+    def __exit__(self, *a):
+        oracle_lib().or_set_accum_double(0)
 
 pytestmark = pytest.mark.gpu
 
@@ -60,6 +79,7 @@ def test_bloom7b1_width_batched_graph_decode_to_ctx2048(B):
     max_ctx = checkpoints[-1] + 1
     gs = Stage(h, nh, L, V, 0, L, dtype="bf16", max_batch=B, max_ctx=max_ctx, max_tokens=B * P, seed=51)
     os_ = OracleStage(h, nh, L, V, 0, L, bf16=True, max_batch=B, max_ctx=max_ctx, seed=51)
+    od = OracleStage(h, nh, L, V, 0, L, bf16=True, max_batch=B, max_ctx=max_ctx, seed=51)  # float64 accumulation
     ids = gen_np.prompt_ids(57, B, P, V).astype(np.int32)
     dev = torch.device("cuda", 0)
     cs = torch.cuda.Stream()
@@ -69,8 +89,10 @@ def test_bloom7b1_width_batched_graph_decode_to_ctx2048(B):
         lg = torch.empty((B, V), dtype=torch.float32, device=dev)
         gs.forward(tin, tok, B, P, slot=0, past_len=0, logits=lg, stream=cs.cuda_stream)
         to, lo = os_.forward(ids, B, P, want_logits=True)
+        with _Accum64():
+            _, ld = od.forward(ids, B, P, want_logits=True)
         cs.synchronize()
-        check_logits_wide(lg.cpu().numpy(), lo, f"B={B} prefill")
+        check_logits_wide(lg.cpu().numpy(), lo, ld, f"B={B} prefill")
         assert_ids_match(tok.cpu().numpy(), to, lo, f"B={B} prefill")
         for layer in range(L):  # the prompt's cache: device prefill epilogue vs the checker
             for r in (0, B // 2, B - 1):
@@ -83,14 +105,18 @@ def test_bloom7b1_width_batched_graph_decode_to_ctx2048(B):
                 gs.forward(tok, tok, B, 1, slot=0, past_len=past, stream=cs.cuda_stream)
                 past += 1
             cs.synchronize()
-            for layer in range(L):  # hand the device cache written since the last checkpoint to the checker
+            for layer in range(L):  # hand the device cache written since the last checkpoint to the checkers
                 for r in range(B):
-                    os_.write_kv(layer, r, synced, gs.read_kv(layer, r, synced, past - synced))
+                    kv = gs.read_kv(layer, r, synced, past - synced)
+                    os_.write_kv(layer, r, synced, kv)
+                    od.write_kv(layer, r, synced, kv)
             t_in = tok.cpu().numpy()
             gs.forward(tok, tok, B, 1, slot=0, past_len=past, logits=lg, stream=cs.cuda_stream)
             to, lo = os_.forward(t_in.reshape(B, 1), B, 1, past_len=past, want_logits=True)
+            with _Accum64():
+                _, ld = od.forward(t_in.reshape(B, 1), B, 1, past_len=past, want_logits=True)
             cs.synchronize()
-            err = check_logits_wide(lg.cpu().numpy(), lo, f"B={B} decode at ctx {ctx}")
+            err = check_logits_wide(lg.cpu().numpy(), lo, ld, f"B={B} decode at ctx {ctx}")
             assert_ids_match(tok.cpu().numpy(), to, lo, f"B={B} decode at ctx {ctx}")
             for layer in range(L):  # the position this step appended: device QKV epilogue vs the checker
                 for r in (0, B - 1):
@@ -101,6 +127,7 @@ def test_bloom7b1_width_batched_graph_decode_to_ctx2048(B):
             synced = past  # the checker computed this position itself
     gs.close()
     os_.close()
+    od.close()
 
 
 @pytest.mark.parametrize("h,nh", [(4096, 32), (2560, 32)])

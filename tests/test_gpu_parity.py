@@ -14,6 +14,7 @@ Tolerances (BASELINE.json north_star):
              the fp32 checker on a bloom-7b1-width block and the GPU 0.017 / 0.0034 (tools/diag_parity.py,
              DESIGN.md section 2): the error is the rounding noise of the format, not of the kernels.
 """
+import json
 import os
 
 import numpy as np
@@ -41,14 +42,31 @@ def pair(h, nh, L, V, lb, le, dtype, seed=0, max_batch=1, max_ctx=128, max_token
     return g, o
 
 
+def record_error(what, got, ref, bound, kind):
+    """Append this check's achieved error and its bound to the parity log (JSON lines; $BS_PARITY_LOG, default
+    gpurun_out/parity_errors.jsonl), so the margin to every bound is on record, not only pass/fail."""
+    d = np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64))
+    rec = {"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], "check": what, "kind": kind,
+           "max_abs": float(d.max()) if d.size else 0.0, "mean_abs": float(d.mean()) if d.size else 0.0,
+           "max_ref": float(np.abs(ref).max()) if np.size(ref) else 0.0, "bound": float(bound)}
+    path = os.environ.get("BS_PARITY_LOG") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                         "gpurun_out", "parity_errors.jsonl")
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    except OSError:
+        pass
+    return rec["max_abs"]
+
+
 def check_close(got, ref, dtype, what=""):
-    err = float(np.abs(got - ref).max())
     if dtype == "bf16":
         tol = BF16_TOL + 2.0 ** -9 * float(np.abs(ref).max())
-        assert err <= tol, f"{what}: max-abs {err} > {tol}"
     else:
-        scale = float(np.abs(ref).max())
-        assert err <= FP32_REL * scale, f"{what}: max-abs {err} > {FP32_REL} * {scale}"
+        tol = FP32_REL * float(np.abs(ref).max())
+    err = record_error(what, got, ref, tol, f"hidden {dtype}")
+    assert err <= tol, f"{what}: max-abs {err} > {tol}"
     return err
 
 
@@ -57,22 +75,19 @@ def check_bf16_stored(got, ref, what=""):
     largest |ref|.  Two correct paths whose fp32 pre-rounding values straddle a rounding boundary store
     adjacent bf16 numbers, a full ulp apart (2^-7 relative: 0.03125 for a cached value in [4, 8), which
     the first bloom-7b1-width prefill measured), so the half-ulp term of check_close is one flip short."""
-    err = float(np.abs(got - ref).max())
     mx = float(np.abs(ref).max())
     ulp = 2.0 ** (np.floor(np.log2(mx)) - 7) if mx > 0 else 0.0
     tol = BF16_TOL + 2.0 ** -9 * mx + ulp
+    err = record_error(what, got, ref, tol, "kv bf16")
     assert err <= tol, f"{what}: max-abs {err} > {tol}"
     return err
 
 
 def check_logits(got, ref, dtype, what=""):
     """Logits: north_star's flat 2e-2 max-abs in bf16 (relative 1e-3 in fp32)."""
-    err = float(np.abs(got - ref).max())
-    if dtype == "bf16":
-        assert err <= BF16_TOL, f"{what}: logits max-abs {err} > {BF16_TOL}"
-    else:
-        scale = float(np.abs(ref).max())
-        assert err <= FP32_REL * scale, f"{what}: max-abs {err} > {FP32_REL} * {scale}"
+    tol = BF16_TOL if dtype == "bf16" else FP32_REL * float(np.abs(ref).max())
+    err = record_error(what, got, ref, tol, f"logits {dtype}")
+    assert err <= tol, f"{what}: logits max-abs {err} > {tol}"
     return err
 
 

@@ -43,19 +43,22 @@ def _worker(rank, world, port, q, head_split):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("head_split", [False, True])
-def test_serve_two_ranks_matches_per_sample_oracle(head_split):
+@pytest.mark.parametrize("world,head_split", [(2, False), (2, True), (3, True), (3, False)])
+def test_serve_two_ranks_matches_per_sample_oracle(world, head_split):
+    """Admission prefill passes (Pipeline.prefill_row) interleaved with the decode rounds: the first token
+    returns on its own communicator -- from the last rank, or from the head ring's closer (rank 1 at world 3,
+    rank 0 itself at world 2)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, head_split)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, head_split)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res["num_sample"] == 5 and res["stages"] == 2 and len(res["samples"]) == 5
+    assert res["num_sample"] == 5 and res["stages"] == world and len(res["samples"]) == 5
     assert res["samples"] == _reference(synthetic_prompts(CFG, MODEL.vocab), CFG.max_length)
 
 
@@ -75,10 +78,27 @@ def test_serve_ragged_prompts_continuous_admission():
     cfg = RunConfig(**{**CFG.__dict__, "num_sample": 6, "core_pool_size": 3, "max_length": 5})
     res = run_rank(cfg, 0, 1, torch.device("cpu"), prompts=prompts, executor_factory=OracleExecutor)
     assert res["samples"] == _reference(prompts, 5)
-    # the admission schedule: the sample after the 1-token prompt starts on that row at round 5
+    # the admission schedule: with the prompt as one prefill pass every sample holds its row max_length - 1
+    # decode rounds, so the fourth sample takes row 0 at round 4; fed a token a round (prefill=False) it
+    # takes the row the 1-token prompt frees, at round 5
     from distributed_inference_demo_amd.serve import admission_schedule
     sched, T = admission_schedule([5, 1, 9, 3, 2, 7], 5, 3)
-    assert sched[:4] == [(0, 0), (1, 0), (2, 0), (1, 5)] and T == res["rounds"]
+    assert sched[:4] == [(0, 0), (1, 0), (2, 0), (0, 4)] and T == res["rounds"]
+    sched, T = admission_schedule([5, 1, 9, 3, 2, 7], 5, 3, prefill=False)
+    assert sched[:4] == [(0, 0), (1, 0), (2, 0), (1, 5)]
+    cfg1 = RunConfig(**{**cfg.__dict__, "prefill": False})
+    res1 = run_rank(cfg1, 0, 1, torch.device("cpu"), prompts=prompts, executor_factory=OracleExecutor)
+    assert res1["samples"] == res["samples"] and res1["rounds"] == T
+
+
+def test_serve_max_length_one_is_prefill_only():
+    """max_length = 1: every sample is its prefill pass alone (no decode round); rows are reused within the
+    same round."""
+    rng = np.random.default_rng(9)
+    prompts = [rng.integers(0, MODEL.vocab, size=n).tolist() for n in (3, 6, 2)]
+    cfg = RunConfig(**{**CFG.__dict__, "num_sample": 3, "core_pool_size": 2, "max_length": 1})
+    res = run_rank(cfg, 0, 1, torch.device("cpu"), prompts=prompts, executor_factory=OracleExecutor)
+    assert res["rounds"] == 0 and res["samples"] == _reference(prompts, 1)
 
 
 def test_serve_rejects_empty_prompts():
