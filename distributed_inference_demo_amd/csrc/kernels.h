@@ -77,6 +77,12 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
                       const Epi& ep, hipStream_t s, const float* stats = nullptr);
 // Do the batched GEMVs publish / consume LayerNorm statistics at this shape (bf16 weights, M rows, K = h)?
 bool linear_ln_stats_supported(int M, int K);
+// Columns per statistics unit of the residual GEMV producing M rows of width N from K inputs (its block width).
+int ln_stats_unit_cols(int M, int N, int K);
+// The statistics of M fp32 rows [M][K] in units of `cw` columns into ep.ln_stats (ep's ln_* fields), bit for
+// bit what a residual GEMV with cw-column blocks publishes: a stage's first layer normalises its hop input
+// exactly as the same layer inside one stage would.
+void launch_ln_stats(const float* x, int M, int K, int cw, const Epi& ep, hipStream_t s);
 
 // The first stage's layer 0 at M <= 2 (bf16): word_embeddings[ids] -> word_embeddings_layernorm (fp32,
 // stored to x_out: the residual stream) -> LN_in -> weight GEMV, one kernel.  False: not launched.

@@ -898,45 +898,28 @@ __device__ __forceinline__ void q8x16_to_bf16(const u32x4v raw, bf16x8& lo, bf16
   }
 }
 
-// EPI_RESID epilogue of a batched GEMV that also publishes the LayerNorm statistics of its output rows
-// (Epi::ln_stats), so the next GEMV can normalise while it stages them and no LayerNorm launch runs
-// between the two (dense -> LN_post + fc1, fc2 -> the next LN_in + QKV or ln_f + lm_head).
-// Per row m the block's columns give (mean_b, M2_b = sum (y - mean_b)^2), written write-through; the
-// block drawing the launch's last ticket (MI355X_MICROARCH.md "Valid forms" row 1: sc1 stores, vmcnt(0),
-// barrier, one agent-scope add; the last adder reads with sc1 loads) combines them in block order:
-// mean = sum n_b mean_b / N, var = sum (M2_b + n_b (mean_b - mean)^2) / N (Chan's pairwise update, no
-// cancellation), and writes (mean, rstd).  Deterministic: fixed block order and wave reductions.
-template <int T, int MT, int WAVES, int ITER>
-__device__ __forceinline__ void tiles_resid_ln_stats(const float (&vs)[ITER], float* red, int M, int N, int n0,
-                                                     const Epi& ep) {
-  constexpr int CW = T * 16, CS = CW + 1, TOTAL = T * 16 * MT * 16, NTH = WAVES * 64;
-  static_assert(CW <= 64, "one wave lane per column of the block");
+// The (mean, M2) of one row's values over one unit of cols <= 64 columns (lane l holds column l, 0 beyond),
+// stored write-through at ln_part[m][unit = blockIdx.x].  The one formula for both producers of statistics
+// (a residual GEMV's epilogue, ln_stats_kernel), so a stage fed its input over a hop normalises bit for bit
+// as the same layer does inside one stage.
+__device__ __forceinline__ void ln_unit_partial(float y, int cols, int m, const Epi& ep) {
+  const int lane = threadIdx.x & 63;
+  const float mb = wave_sum(y) / (float)cols;
+  const float d = lane < cols ? y - mb : 0.f;
+  const float m2 = wave_sum(d * d);
+  if (lane == 0) {
+    const __amdgpu_buffer_rsrc_t part = attn_rsrc(ep.ln_part);
+    const uint32_t off = (uint32_t)(((size_t)m * ep.ln_nblk + blockIdx.x) * 2) * 4;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mb), part, off, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m2), part, off + 4, 0, 16);
+  }
+}
+
+// Arrival ticket of the launch's gridDim.x units; the last arriver combines every row's unit partials in unit
+// order (units of CW columns, the last one ragged) and writes ln_stats.
+template <int WAVES>
+__device__ void ln_arrive_and_combine(int M, int N, int CW, const Epi& ep) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();  // every thread has read its partial tiles out of `red`
-#pragma unroll
-  for (int it = 0; it < ITER; it++) {
-    const int idx = it * NTH + threadIdx.x;
-    const int nl = idx % CW, ml = idx / CW, n = n0 + nl;
-    if (idx < TOTAL && ml < M && n < N) {
-      const float y = resid_out<bf16>(ep, ml, n, vs[it]);
-      ep.out_f32[(size_t)ml * ep.ldo + n] = y;
-      red[ml * CS + nl] = y;
-    }
-  }
-  __syncthreads();
-  const int cols = min(CW, N - n0);
-  const __amdgpu_buffer_rsrc_t part = attn_rsrc(ep.ln_part);
-  for (int m = w; m < M; m += WAVES) {
-    const float y = lane < cols ? red[m * CS + lane] : 0.f;
-    const float mb = wave_sum(y) / (float)cols;
-    const float d = lane < cols ? y - mb : 0.f;
-    const float m2 = wave_sum(d * d);
-    if (lane == 0) {
-      const uint32_t off = (uint32_t)(((size_t)m * ep.ln_nblk + blockIdx.x) * 2) * 4;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mb), part, off, 0, 16);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m2), part, off + 4, 0, 16);
-    }
-  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __shared__ int ln_last;
   __syncthreads();
@@ -948,6 +931,7 @@ __device__ __forceinline__ void tiles_resid_ln_stats(const float (&vs)[ITER], fl
   }
   __syncthreads();
   if (!ln_last) return;
+  const __amdgpu_buffer_rsrc_t part = attn_rsrc(ep.ln_part);
   // every partial of the wave's rows requested at once (one memory round trip), then combined
   constexpr int RPW = (32 + WAVES - 1) / WAVES, NBK = 4;  // rows per wave (M <= 32), blocks per lane (<= 256)
   const int nb = gridDim.x;
@@ -987,6 +971,47 @@ __device__ __forceinline__ void tiles_resid_ln_stats(const float (&vs)[ITER], fl
       ep.ln_stats[2 * m + 1] = 1.0f / sqrtf(var + ep.ln_eps);
     }
   }
+}
+
+// EPI_RESID epilogue of a batched GEMV that also publishes the LayerNorm statistics of its output rows
+// (Epi::ln_stats), so the next GEMV can normalise while it stages them and no LayerNorm launch runs
+// between the two (dense -> LN_post + fc1, fc2 -> the next LN_in + QKV or ln_f + lm_head).
+// Per row m the block's columns give (mean_b, M2_b = sum (y - mean_b)^2), written write-through; the
+// block drawing the launch's last ticket (MI355X_MICROARCH.md "Valid forms" row 1: sc1 stores, vmcnt(0),
+// barrier, one agent-scope add; the last adder reads with sc1 loads) combines them in block order:
+// mean = sum n_b mean_b / N, var = sum (M2_b + n_b (mean_b - mean)^2) / N (Chan's pairwise update, no
+// cancellation), and writes (mean, rstd).  Deterministic: fixed block order and wave reductions.
+template <int T, int MT, int WAVES, int ITER>
+__device__ __forceinline__ void tiles_resid_ln_stats(const float (&vs)[ITER], float* red, int M, int N, int n0,
+                                                     const Epi& ep) {
+  constexpr int CW = T * 16, CS = CW + 1, TOTAL = T * 16 * MT * 16, NTH = WAVES * 64;
+  static_assert(CW <= 64, "one wave lane per column of the block");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();  // every thread has read its partial tiles out of `red`
+#pragma unroll
+  for (int it = 0; it < ITER; it++) {
+    const int idx = it * NTH + threadIdx.x;
+    const int nl = idx % CW, ml = idx / CW, n = n0 + nl;
+    if (idx < TOTAL && ml < M && n < N) {
+      const float y = resid_out<bf16>(ep, ml, n, vs[it]);
+      ep.out_f32[(size_t)ml * ep.ldo + n] = y;
+      red[ml * CS + nl] = y;
+    }
+  }
+  __syncthreads();
+  const int cols = min(CW, N - n0);
+  for (int m = w; m < M; m += WAVES) ln_unit_partial(lane < cols ? red[m * CS + lane] : 0.f, cols, m, ep);
+  ln_arrive_and_combine<WAVES>(M, N, CW, ep);
+}
+
+// LayerNorm statistics of M fp32 rows [M][K] in units of CW columns -- exactly what a residual GEMV with
+// CW-column blocks publishes (the same two functions) -- for a stage's first layer, whose input came over a
+// hop or from the embedding: block = one unit, 4 waves over the rows.
+__global__ __launch_bounds__(256) void ln_stats_kernel(const float* __restrict__ x, int M, int K, int CW, Epi ep) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * CW, cols = min(CW, K - c0);
+  for (int m = w; m < M; m += 4) ln_unit_partial(lane < cols ? x[(size_t)m * K + c0 + lane] : 0.f, cols, m, ep);
+  ln_arrive_and_combine<4>(M, K, CW, ep);
 }
 
 // Tile GEMV epilogue: every wave's partial tiles meet in LDS (`red`, [WAVES][T*16][MT*16+1]); split-K
@@ -1358,16 +1383,22 @@ static const TileCfg kTileTable[] = {
 
 // lx (bf16 weights): the activations are LayerNorm(lx->x) (gemv_ldsw4's XLN); false when gemv_ldsw4 does not
 // take the shape (the caller runs the LayerNorm itself).
+// (T, KS, waves) of the table for an M-row (N, K) batched GEMV (WV = 0: not in the table).
+static void tiles_plan(int M, int N, int K, int* T, int* KS, int* WV) {
+  *T = N >= 16384 ? 4 : 2; *KS = 1; *WV = 0;
+  for (const TileCfg& c : kTileTable)
+    if (c.N == N && c.K == K) {
+      *T = M > 16 ? c.T2 : c.T1; *KS = M > 16 ? c.KS2 : c.KS1; *WV = M > 16 ? c.W2 : c.W1;
+    }
+}
+
 template <typename WT = bf16>
 static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K, const Epi& ep, hipStream_t s,
                                 const LnX* lx = nullptr) {
   if (M <= 4 || M > 32 || (K % 64) != 0) return false;
   const int units = K / 64;
-  int T = N >= 16384 ? 4 : 2, KS = 1, WV = 0;
-  for (const TileCfg& c : kTileTable)
-    if (c.N == N && c.K == K) {
-      T = M > 16 ? c.T2 : c.T1; KS = M > 16 ? c.KS2 : c.KS1; WV = M > 16 ? c.W2 : c.W1;
-    }
+  int T, KS, WV;
+  tiles_plan(M, N, K, &T, &KS, &WV);
   const int blocks = (N + T * 16 - 1) / (T * 16);
   const bool sk_ok = ep.sk_ws && ep.sk_tickets && blocks <= ep.sk_ntickets;
   if (WV == 0) {  // not in the table
@@ -2213,6 +2244,17 @@ static void gemv_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, int M,
 
 // LN(x) -> weight GEMM.  bf16 with M <= 8: LayerNorm fused into the GEMV prologue.  Otherwise a
 // LayerNorm kernel writes the normalised activations to `xn_scratch` first.
+int ln_stats_unit_cols(int M, int N, int K) {
+  int T, KS, WV;
+  tiles_plan(M, N, K, &T, &KS, &WV);
+  return T * 16;
+}
+
+void launch_ln_stats(const float* x, int M, int K, int cw, const Epi& ep, hipStream_t s) {
+  if (M <= 0) return;
+  ln_stats_kernel<<<(K + cw - 1) / cw, 256, 0, s>>>(x, M, K, cw, ep);
+}
+
 bool linear_ln_stats_supported(int M, int K) {
   // every batched GEMV of the layer (N = h or 4h outputs, K = h or 4h) runs tiles_epilogue, and a
   // producer's epilogue grid (<= K / 16 blocks for N = K = h) fits tiles_resid_ln_stats' 256 partials

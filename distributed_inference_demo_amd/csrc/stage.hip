@@ -1134,9 +1134,14 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
                                w.t[T_QKV_W], M, 3 * h, h, with_splitk(s, e), st);
       if (!done) launch_layernorm(s->bf16, s->wemb, ids, 0, 0, s->emb_g, s->emb_b, s->xa, 1, M, h, d.ln_eps, st);
     }
-    if (!done)
+    if (!done) {
+      // the first layer's input came over the hop (or from the embedding): its statistics in the units the
+      // fc2 GEMV publishes them in, so the layer normalises bit for bit as it would inside one stage
+      if (lnfuse && l == 0)
+        launch_ln_stats(cur, M, h, ln_stats_unit_cols(M, h, 4 * h), with_ln_stats(s, Epi{}, s->lnst[0]), st);
       wlinear_ln(s, st, cur, w.t[T_LN1_G], w.t[T_LN1_B], w, T_QKV_W, M, 3 * h, h, with_splitk(s, e), 4,
-                 lnfuse && l > 0 ? s->lnst[0] : nullptr);
+                 lnfuse ? s->lnst[0] : nullptr);
+    }
     // attention
     AttnArgs a{};
     a.q = s->q; a.k_cache = kbase; a.v_cache = kbase + s->kv_half; a.ctx_out = s->ctx; a.slopes = s->slopes;

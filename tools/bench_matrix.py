@@ -61,7 +61,11 @@ def run(name, B, P, K, W=4):
             "prefill_TFLOPs": config.prefill_flops(m, m.n_layer, B, P, True) / tp / 1e12}
 
 
+BATCHED = [("bloom-1b1", 8, 128, 64), ("bloom-1b1", 32, 128, 64), ("bloom-560m", 16, 16, 128), ("bloom-560m", 32, 16, 128),
+           ("bloom-3b", 8, 64, 128), ("bloom-3b", 32, 64, 64), ("bloom-7b1", 16, 128, 64), ("bloom-7b1", 32, 128, 64),
+           ("bloom-7b1", 32, 1024, 32)]
+
 if __name__ == "__main__":
-    cfgs = CONFIGS[:3] if "--quick" in sys.argv else CONFIGS
+    cfgs = CONFIGS[:3] if "--quick" in sys.argv else (BATCHED if "batched" in sys.argv else CONFIGS)
     for c in cfgs:
         print(json.dumps(run(*c)), flush=True)
