@@ -41,16 +41,6 @@ struct Epi {
   // int8 weights: y[m][n] *= col_scale[n] before the epilogue (the weight operand held Q, not
   // Q * scale).  Null otherwise.  Not applied by EPI_ARGMAX.
   const float* col_scale;
-  // EPI_RESID in the batched GEMVs (4 < M <= 32, tiles_epilogue): also publish the LayerNorm statistics of
-  // the output rows, ln_stats [M][2] = (mean, 1 / sqrt(var + ln_eps)), for the consumer GEMV that applies
-  // the LayerNorm while staging its activations (launch_linear_ln's `stats`).  Each epilogue block writes
-  // its columns' (mean, M2) to ln_part [M][ln_nblk][2]; the last arriver (ln_ticket, zero between
-  // launches) combines them in block order.  Null ln_stats: not computed.
-  float* ln_stats;
-  float* ln_part;
-  unsigned* ln_ticket;
-  int ln_nblk;
-  float ln_eps;
 };
 
 // dtype tag: 0 = fp32, 1 = bf16
@@ -70,19 +60,9 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
                    hipStream_t s);
 
 // LayerNorm(x rows) followed by a weight GEMM; fused into one kernel on the bf16 decode path.
-// `stats` (optional, [M][2] (mean, rstd) published by the producer of x through Epi::ln_stats): the batched
-// GEMV (4 < M <= 32, contiguous rows) applies the LayerNorm while staging x, with no LayerNorm launch.
 void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offset, const void* gamma,
                       const void* beta, float eps, void* xn_scratch, const void* W, int M, int N, int K,
-                      const Epi& ep, hipStream_t s, const float* stats = nullptr);
-// Do the batched GEMVs publish / consume LayerNorm statistics at this shape (bf16 weights, M rows, K = h)?
-bool linear_ln_stats_supported(int M, int K);
-// Columns per statistics unit of the residual GEMV producing M rows of width N from K inputs (its block width).
-int ln_stats_unit_cols(int M, int N, int K);
-// The statistics of M fp32 rows [M][K] in units of `cw` columns into ep.ln_stats (ep's ln_* fields), bit for
-// bit what a residual GEMV with cw-column blocks publishes: a stage's first layer normalises its hop input
-// exactly as the same layer inside one stage would.
-void launch_ln_stats(const float* x, int M, int K, int cw, const Epi& ep, hipStream_t s);
+                      const Epi& ep, hipStream_t s);
 
 // The first stage's layer 0 at M <= 2 (bf16): word_embeddings[ids] -> word_embeddings_layernorm (fp32,
 // stored to x_out: the residual stream) -> LN_in -> weight GEMV, one kernel.  False: not launched.

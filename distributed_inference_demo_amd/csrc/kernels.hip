@@ -191,13 +191,6 @@ __device__ __forceinline__ void epi_store(const Epi& e, int m, int n, float v) {
   }
 }
 
-// EPI_RESID's output value (epi_store's arithmetic), for the epilogue that also takes LayerNorm statistics.
-template <typename T>
-__device__ __forceinline__ float resid_out(const Epi& e, int m, int n, float v) {
-  if (e.col_scale) v *= e.col_scale[n];
-  return (v + to_f32(((const T*)e.bias)[n])) + e.resid[(size_t)m * e.ldo + n];
-}
-
 // Epilogue operands that do not depend on the GEMV result (bias, residual, past_len): a GEMV whose
 // output lane is known up front loads them at kernel start, so the epilogue is not one more memory
 // round trip after the reduction (decode GEMVs are latency-bound; each round trip is ~1 us).
@@ -898,122 +891,6 @@ __device__ __forceinline__ void q8x16_to_bf16(const u32x4v raw, bf16x8& lo, bf16
   }
 }
 
-// The (mean, M2) of one row's values over one unit of cols <= 64 columns (lane l holds column l, 0 beyond),
-// stored write-through at ln_part[m][unit = blockIdx.x].  The one formula for both producers of statistics
-// (a residual GEMV's epilogue, ln_stats_kernel), so a stage fed its input over a hop normalises bit for bit
-// as the same layer does inside one stage.
-__device__ __forceinline__ void ln_unit_partial(float y, int cols, int m, const Epi& ep) {
-  const int lane = threadIdx.x & 63;
-  const float mb = wave_sum(y) / (float)cols;
-  const float d = lane < cols ? y - mb : 0.f;
-  const float m2 = wave_sum(d * d);
-  if (lane == 0) {
-    const __amdgpu_buffer_rsrc_t part = attn_rsrc(ep.ln_part);
-    const uint32_t off = (uint32_t)(((size_t)m * ep.ln_nblk + blockIdx.x) * 2) * 4;
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mb), part, off, 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m2), part, off + 4, 0, 16);
-  }
-}
-
-// Arrival ticket of the launch's gridDim.x units; the last arriver combines every row's unit partials in unit
-// order (units of CW columns, the last one ragged) and writes ln_stats.
-template <int WAVES>
-__device__ void ln_arrive_and_combine(int M, int N, int CW, const Epi& ep) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __shared__ int ln_last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    typedef __attribute__((address_space(1))) unsigned gu32;
-    const unsigned old = __hip_atomic_fetch_add((gu32*)ep.ln_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ln_last = old == gridDim.x - 1;
-    if (ln_last) __hip_atomic_store((gu32*)ep.ln_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!ln_last) return;
-  const __amdgpu_buffer_rsrc_t part = attn_rsrc(ep.ln_part);
-  // every partial of the wave's rows requested at once (one memory round trip), then combined
-  constexpr int RPW = (32 + WAVES - 1) / WAVES, NBK = 4;  // rows per wave (M <= 32), blocks per lane (<= 256)
-  const int nb = gridDim.x;
-  float pm[RPW][NBK], p2[RPW][NBK];
-#pragma unroll
-  for (int i = 0; i < RPW; i++) {
-    const int m = min(w + i * WAVES, M - 1);
-#pragma unroll
-    for (int k = 0; k < NBK; k++) {
-      const int b = min(lane + 64 * k, nb - 1);
-      const uint32_t off = (uint32_t)(((size_t)m * ep.ln_nblk + b) * 2) * 4;
-      const uint2 v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(part, off, 0, 16));
-      pm[i][k] = __uint_as_float(v.x);
-      p2[i][k] = __uint_as_float(v.y);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < RPW; i++) {
-    const int m = w + i * WAVES;
-    if (m >= M) break;  // wave-uniform
-    float sum = 0.f, q = 0.f;
-#pragma unroll
-    for (int k = 0; k < NBK; k++) {
-      const int b = lane + 64 * k;
-      if (b < nb) sum += (float)min(CW, N - b * CW) * pm[i][k];
-    }
-    const float mean = wave_sum(sum) / (float)N;
-#pragma unroll
-    for (int k = 0; k < NBK; k++) {
-      const int b = lane + 64 * k;
-      const float dd = pm[i][k] - mean;
-      if (b < nb) q += p2[i][k] + (float)min(CW, N - b * CW) * dd * dd;
-    }
-    const float var = wave_sum(q) / (float)N;
-    if (lane == 0) {
-      ep.ln_stats[2 * m] = mean;
-      ep.ln_stats[2 * m + 1] = 1.0f / sqrtf(var + ep.ln_eps);
-    }
-  }
-}
-
-// EPI_RESID epilogue of a batched GEMV that also publishes the LayerNorm statistics of its output rows
-// (Epi::ln_stats), so the next GEMV can normalise while it stages them and no LayerNorm launch runs
-// between the two (dense -> LN_post + fc1, fc2 -> the next LN_in + QKV or ln_f + lm_head).
-// Per row m the block's columns give (mean_b, M2_b = sum (y - mean_b)^2), written write-through; the
-// block drawing the launch's last ticket (MI355X_MICROARCH.md "Valid forms" row 1: sc1 stores, vmcnt(0),
-// barrier, one agent-scope add; the last adder reads with sc1 loads) combines them in block order:
-// mean = sum n_b mean_b / N, var = sum (M2_b + n_b (mean_b - mean)^2) / N (Chan's pairwise update, no
-// cancellation), and writes (mean, rstd).  Deterministic: fixed block order and wave reductions.
-template <int T, int MT, int WAVES, int ITER>
-__device__ __forceinline__ void tiles_resid_ln_stats(const float (&vs)[ITER], float* red, int M, int N, int n0,
-                                                     const Epi& ep) {
-  constexpr int CW = T * 16, CS = CW + 1, TOTAL = T * 16 * MT * 16, NTH = WAVES * 64;
-  static_assert(CW <= 64, "one wave lane per column of the block");
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();  // every thread has read its partial tiles out of `red`
-#pragma unroll
-  for (int it = 0; it < ITER; it++) {
-    const int idx = it * NTH + threadIdx.x;
-    const int nl = idx % CW, ml = idx / CW, n = n0 + nl;
-    if (idx < TOTAL && ml < M && n < N) {
-      const float y = resid_out<bf16>(ep, ml, n, vs[it]);
-      ep.out_f32[(size_t)ml * ep.ldo + n] = y;
-      red[ml * CS + nl] = y;
-    }
-  }
-  __syncthreads();
-  const int cols = min(CW, N - n0);
-  for (int m = w; m < M; m += WAVES) ln_unit_partial(lane < cols ? red[m * CS + lane] : 0.f, cols, m, ep);
-  ln_arrive_and_combine<WAVES>(M, N, CW, ep);
-}
-
-// LayerNorm statistics of M fp32 rows [M][K] in units of CW columns -- exactly what a residual GEMV with
-// CW-column blocks publishes (the same two functions) -- for a stage's first layer, whose input came over a
-// hop or from the embedding: block = one unit, 4 waves over the rows.
-__global__ __launch_bounds__(256) void ln_stats_kernel(const float* __restrict__ x, int M, int K, int CW, Epi ep) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c0 = blockIdx.x * CW, cols = min(CW, K - c0);
-  for (int m = w; m < M; m += 4) ln_unit_partial(lane < cols ? x[(size_t)m * K + c0 + lane] : 0.f, cols, m, ep);
-  ln_arrive_and_combine<4>(M, K, CW, ep);
-}
-
 // Tile GEMV epilogue: every wave's partial tiles meet in LDS (`red`, [WAVES][T*16][MT*16+1]); split-K
 // blocks publish write-through partials and the last arriver sums them in split order; then the epilogue.
 template <int T, int MT, int WAVES>
@@ -1082,10 +959,6 @@ __device__ __forceinline__ void tiles_epilogue(const f32x4 (&acc)[T][MT], float*
       }
       vs[it] = v;
     }
-  }
-  if (ep.kind == EPI_RESID && ep.ln_stats) {
-    tiles_resid_ln_stats<T, MT, WAVES, ITER>(vs, red, M, N, n0, ep);
-    return;
   }
   epi_dispatch(ep.kind, [&](auto kc) {
     constexpr int EK = decltype(kc)::value;
@@ -1205,19 +1078,9 @@ __device__ __forceinline__ bf16x8 q8x8_to_bf16(const uint2 raw) {
 
 // WT = bf16 (KC = 64 columns = 128 B per row per stage) or int8_t (KC = 128 columns = 128 B; each A fragment
 // is 8 bytes converted in registers, the row scale applied by the epilogue's col_scale).
-// XLN: the activations are LayerNorm(x) of fp32 rows x [M][K] with the statistics their producer published
-// (Epi::ln_stats): each stage's fragments are loaded as fp32 with gamma / beta and normalised to bf16 in
-// registers ((x - mean) * rstd * gamma + beta, ln_rows_finish's arithmetic) just before their MFMAs.
-struct LnX {
-  const float* x;      // fp32 rows [M][K]
-  const float* stats;  // [M][2] (mean, rstd)
-  const bf16* gamma;
-  const bf16* beta;
-};
-
-template <int T, int WAVES, int MT, typename WT = bf16, bool XLN = false>
+template <int T, int WAVES, int MT, typename WT = bf16>
 __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __restrict__ W, const bf16* __restrict__ X,
-                                                               int M, int N, int K, Epi ep, LnX lx) {
+                                                               int M, int N, int K, Epi ep) {
   constexpr int RB = 128, KC = RB / (int)sizeof(WT);  // bytes / columns of one row per stage
   constexpr int CPR = RB / 16, RPI = 64 / CPR, ROWS = T * 16, NI = ROWS / RPI, KSTEP = KC / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1237,73 +1100,21 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
     return row * RB + ((((byte >> 4) ^ (row & (CPR - 1)))) << 4) + (byte & 15);
   };
   const bf16* xsrc[MT];
-  const float* xfsrc[MT];
-  float mean[MT], rstd[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; mt++) {
-    const int row = min(mt * 16 + r, M - 1);
-    if constexpr (XLN) {
-      xfsrc[mt] = lx.x + (size_t)row * K + kbeg + g * 8;
-      mean[mt] = lx.stats[2 * row];
-      rstd[mt] = lx.stats[2 * row + 1];
-    } else {
-      xsrc[mt] = X + (size_t)row * K + kbeg + g * 8;
-    }
-  }
+  for (int mt = 0; mt < MT; mt++) xsrc[mt] = X + (size_t)min(mt * 16 + r, M - 1) * K + kbeg + g * 8;
   u32x4v wr[2][NI];
   bf16x8 xr[2][MT][KSTEP];
-  f32x4 xf[XLN ? 2 : 1][MT][KSTEP][2];   // XLN: the raw fp32 activations of a stage
-  u32x4v gbr[XLN ? 2 : 1][KSTEP][2];     // XLN: their gamma, beta (8 bf16 each)
-  auto load = [&](int st, int b) {
+  auto load = [&](int st, u32x4v (&ww)[NI], bf16x8 (&xx)[MT][KSTEP]) {
     const size_t o = (size_t)st * KC;
 #pragma unroll
     for (int i = 0; i < NI; i++) {
       const WT* src = (RPI * i + lr < rows_ok) ? wsrc + i * wstep : wsrc;
-      wr[b][i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(src + o));
+      ww[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(src + o));
     }
-    if constexpr (XLN) {
 #pragma unroll
-      for (int j = 0; j < KSTEP; j++) {
-        const size_t c = kbeg + o + 32 * j + g * 8;
-        gbr[b][j][0] = *reinterpret_cast<const u32x4v*>(lx.gamma + c);
-        gbr[b][j][1] = *reinterpret_cast<const u32x4v*>(lx.beta + c);
-      }
+    for (int mt = 0; mt < MT; mt++)
 #pragma unroll
-      for (int mt = 0; mt < MT; mt++)
-#pragma unroll
-        for (int j = 0; j < KSTEP; j++) {
-          xf[b][mt][j][0] = *reinterpret_cast<const f32x4*>(xfsrc[mt] + o + 32 * j);
-          xf[b][mt][j][1] = *reinterpret_cast<const f32x4*>(xfsrc[mt] + o + 32 * j + 4);
-        }
-    } else {
-#pragma unroll
-      for (int mt = 0; mt < MT; mt++)
-#pragma unroll
-        for (int j = 0; j < KSTEP; j++) xr[b][mt][j] = *reinterpret_cast<const bf16x8*>(xsrc[mt] + o + 32 * j);
-    }
-  };
-  // XLN: normalise stage b's fragments (ln_rows_finish's expression and rounding)
-  auto normalise = [&](int b) {
-    if constexpr (XLN) {
-#pragma unroll
-      for (int j = 0; j < KSTEP; j++) {
-        const u32x4v gr = gbr[b][j][0], br = gbr[b][j][1];
-        const uint32_t gw[4] = {gr.x, gr.y, gr.z, gr.w}, bw[4] = {br.x, br.y, br.z, br.w};
-#pragma unroll
-        for (int mt = 0; mt < MT; mt++) {
-          const f32x4 a0 = xf[b][mt][j][0], a1 = xf[b][mt][j][1];
-          const float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-          bf16x8 o;
-#pragma unroll
-          for (int e = 0; e < 8; e++) {
-            const float gg = __uint_as_float(e & 1 ? gw[e >> 1] & 0xFFFF0000u : gw[e >> 1] << 16);
-            const float bb = __uint_as_float(e & 1 ? bw[e >> 1] & 0xFFFF0000u : bw[e >> 1] << 16);
-            o[e] = (bf16)((v[e] - mean[mt]) * rstd[mt] * gg + bb);
-          }
-          xr[b][mt][j] = o;
-        }
-      }
-    }
+      for (int j = 0; j < KSTEP; j++) xx[mt][j] = *reinterpret_cast<const bf16x8*>(xsrc[mt] + o + 32 * j);
   };
   f32x4 acc[T][MT];
 #pragma unroll
@@ -1311,8 +1122,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
 #pragma unroll
     for (int mt = 0; mt < MT; mt++) acc[t][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   auto stage = [&](int b, int st) {
-    if (st + 1 < nst) load(st + 1, b ^ 1);
-    normalise(b);  // waits for stage b only: the next stage's loads are already in flight
+    if (st + 1 < nst) load(st + 1, wr[b ^ 1], xr[b ^ 1]);
 #pragma unroll
     for (int i = 0; i < NI; i++) *reinterpret_cast<u32x4v*>(&wl[swz(RPI * i + lr, lc * 16)]) = wr[b][i];
     __builtin_amdgcn_wave_barrier();
@@ -1330,7 +1140,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
     __builtin_amdgcn_wave_barrier();
   };
   if (nst > 0) {
-    load(0, 0);
+    load(0, wr[0], xr[0]);
     for (int st = 0; st < nst; st += 2) {
       stage(0, st);
       if (st + 1 < nst) stage(1, st + 1);
@@ -1340,17 +1150,10 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
 }
 
 template <int T, int WAVES, int MT, typename WT>
-static void gemv_ldsw4_launch(const bf16* X, const WT* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s,
-                              const LnX* lx = nullptr) {
+static void gemv_ldsw4_launch(const bf16* X, const WT* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s) {
   const size_t shm = (size_t)WAVES * T * 16 * 128 + sizeof(float) * WAVES * (T * 16) * (MT * 16 + 1);
   const int blocks = (N + T * 16 - 1) / (T * 16);
-  if constexpr (sizeof(WT) == 2) {
-    if (lx) {
-      gemv_ldsw4_kernel<T, WAVES, MT, WT, true><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep, *lx);
-      return;
-    }
-  }
-  gemv_ldsw4_kernel<T, WAVES, MT, WT><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep, LnX{});
+  gemv_ldsw4_kernel<T, WAVES, MT, WT><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
 }
 
 template <int T, int MT, int WAVES, typename WT = bf16>
@@ -1381,24 +1184,15 @@ static const TileCfg kTileTable[] = {
   {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 2, 2, 8, 2, 2, 8},
 };
 
-// lx (bf16 weights): the activations are LayerNorm(lx->x) (gemv_ldsw4's XLN); false when gemv_ldsw4 does not
-// take the shape (the caller runs the LayerNorm itself).
-// (T, KS, waves) of the table for an M-row (N, K) batched GEMV (WV = 0: not in the table).
-static void tiles_plan(int M, int N, int K, int* T, int* KS, int* WV) {
-  *T = N >= 16384 ? 4 : 2; *KS = 1; *WV = 0;
-  for (const TileCfg& c : kTileTable)
-    if (c.N == N && c.K == K) {
-      *T = M > 16 ? c.T2 : c.T1; *KS = M > 16 ? c.KS2 : c.KS1; *WV = M > 16 ? c.W2 : c.W1;
-    }
-}
-
 template <typename WT = bf16>
-static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K, const Epi& ep, hipStream_t s,
-                                const LnX* lx = nullptr) {
+static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K, const Epi& ep, hipStream_t s) {
   if (M <= 4 || M > 32 || (K % 64) != 0) return false;
   const int units = K / 64;
-  int T, KS, WV;
-  tiles_plan(M, N, K, &T, &KS, &WV);
+  int T = N >= 16384 ? 4 : 2, KS = 1, WV = 0;
+  for (const TileCfg& c : kTileTable)
+    if (c.N == N && c.K == K) {
+      T = M > 16 ? c.T2 : c.T1; KS = M > 16 ? c.KS2 : c.KS1; WV = M > 16 ? c.W2 : c.W1;
+    }
   const int blocks = (N + T * 16 - 1) / (T * 16);
   const bool sk_ok = ep.sk_ws && ep.sk_tickets && blocks <= ep.sk_ntickets;
   if (WV == 0) {  // not in the table
@@ -1416,8 +1210,8 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
     if (T <= 4 && K % (KS * 8 * KC) == 0) {
       auto go4 = [&](auto tc) {
         constexpr int TT = decltype(tc)::value;
-        if (two) gemv_ldsw4_launch<TT, 8, 2, WT>(x, w, M, N, K, KS, ep, s, lx);
-        else gemv_ldsw4_launch<TT, 8, 1, WT>(x, w, M, N, K, KS, ep, s, lx);
+        if (two) gemv_ldsw4_launch<TT, 8, 2, WT>(x, w, M, N, K, KS, ep, s);
+        else gemv_ldsw4_launch<TT, 8, 1, WT>(x, w, M, N, K, KS, ep, s);
       };
       if (T == 4) go4(EpiKindC<4>{});
       else if (T == 3) go4(EpiKindC<3>{});
@@ -1426,7 +1220,6 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
       return true;
     }
   }
-  if (lx) return false;
   auto go = [&](auto tc, auto wc) {
     constexpr int TT = decltype(tc)::value, WW = decltype(wc)::value;
     if (two) gemv_tiles_launch<TT, 2, WW, WT>(x, w, M, N, K, KS, ep, s);
@@ -2244,31 +2037,10 @@ static void gemv_dispatch(const bf16* x, const LnArgs& ln, const bf16* w, int M,
 
 // LN(x) -> weight GEMM.  bf16 with M <= 8: LayerNorm fused into the GEMV prologue.  Otherwise a
 // LayerNorm kernel writes the normalised activations to `xn_scratch` first.
-int ln_stats_unit_cols(int M, int N, int K) {
-  int T, KS, WV;
-  tiles_plan(M, N, K, &T, &KS, &WV);
-  return T * 16;
-}
-
-void launch_ln_stats(const float* x, int M, int K, int cw, const Epi& ep, hipStream_t s) {
-  if (M <= 0) return;
-  ln_stats_kernel<<<(K + cw - 1) / cw, 256, 0, s>>>(x, M, K, cw, ep);
-}
-
-bool linear_ln_stats_supported(int M, int K) {
-  // every batched GEMV of the layer (N = h or 4h outputs, K = h or 4h) runs tiles_epilogue, and a
-  // producer's epilogue grid (<= K / 16 blocks for N = K = h) fits tiles_resid_ln_stats' 256 partials
-  return M > 4 && M <= 32 && K % 64 == 0 && K / 16 <= 256;
-}
-
 void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offset, const void* gamma,
                       const void* beta, float eps, void* xn_scratch, const void* W, int M, int N, int K,
-                      const Epi& ep, hipStream_t s, const float* stats) {
+                      const Epi& ep, hipStream_t s) {
   if (M <= 0) return;
-  if (stats && is_bf16 && row_stride == 1 && row_offset == 0 && linear_ln_stats_supported(M, K)) {
-    const LnX lx{x, stats, (const bf16*)gamma, (const bf16*)beta};
-    if (gemv_tiles_dispatch<bf16>(nullptr, (const bf16*)W, M, N, K, ep, s, &lx)) return;
-  }
   // 4 < M <= 32: a LayerNorm kernel + the tile GEMV beats the per-tile LN-fused GEMV
   // (tools/gemv_probe.hip batched section)
   const bool tiles = is_bf16 && M > 4 && M <= 32 && (K % 64) == 0;

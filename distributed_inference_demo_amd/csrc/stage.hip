@@ -76,7 +76,6 @@ struct ProfClass {
 // gemm_split_k's 64x64 split-K tiles.
 constexpr size_t kSkCap = (size_t)1024 * 128 * 128;
 constexpr int kSkTickets = 4096;
-constexpr int kLnRows = 32, kLnBlocks = 256;  // batched-GEMV LayerNorm statistics (tiles_resid_ln_stats)
 
 struct bs_stage {
   bs_stage_desc d;
@@ -124,11 +123,6 @@ struct bs_stage {
   hipStream_t past_stream = nullptr;   // the stream those forwards were enqueued on
   float* sk_ws = nullptr;              // batched-GEMV split-K partials (kSkCap floats)
   unsigned* sk_tickets = nullptr;      // [kSkTickets]
-  // batched decode (4 < M <= 32): LayerNorm statistics published by the residual GEMVs (Epi::ln_stats) --
-  // lnst[0] of the block output x (fc2: the next LN_in / ln_f), lnst[1] of x + attention (dense: LN_post)
-  float* lnst[2] = {nullptr, nullptr};  // [kLnRows][2] each
-  float* ln_part = nullptr;             // [kLnRows][kLnBlocks][2] per-block partials
-  unsigned* ln_ticket = nullptr;
   ProfClass prof;
   std::vector<std::pair<void*, size_t>> order;  // canonical weight order (BS_WEIGHTS_HOST layout)
   std::vector<std::pair<const float*, int>> order_q8;  // per order entry: (row scales, K) if int8, else (null, 0)
@@ -596,9 +590,6 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   wadd((size_t)desc->max_batch * desc->n_head * 4);  // attention split-merge tickets
   wadd(kSkCap * 4);                                  // batched-GEMV split-K partials
   wadd(kSkTickets * 4);                              // and their tickets
-  wadd(2 * kLnRows * 2 * 4);                         // LayerNorm statistics (two vectors)
-  wadd((size_t)kLnRows * kLnBlocks * 2 * 4);         // and their per-block partials
-  wadd(4);                                           // and the arrival ticket
   s->wsbytes = woff;
   if (hipMalloc(&s->ws, s->wsbytes) != hipSuccess) return cleanup(fail(BS_ERR_OOM, "workspace allocation failed"));
   int wi = 0;
@@ -619,10 +610,6 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   s->att_tickets = (unsigned*)(s->ws + wo[wi++]);
   s->sk_ws = (float*)(s->ws + wo[wi++]);
   s->sk_tickets = (unsigned*)(s->ws + wo[wi++]);
-  s->lnst[0] = (float*)(s->ws + wo[wi++]);
-  s->lnst[1] = s->lnst[0] + kLnRows * 2;
-  s->ln_part = (float*)(s->ws + wo[wi++]);
-  s->ln_ticket = (unsigned*)(s->ws + wo[wi++]);
   HIP_TRY(hipMemsetAsync(s->ws, 0, s->wsbytes, s->own));
   // decode engine: bf16 block weights at the arena offsets engine.hip assumes (checked, not trusted)
   if (s->bf16 && !s->q8 && s->L > 0 && (h == 1024 || h == 1536)) {
@@ -990,23 +977,15 @@ static void linear(bs_stage* s, hipStream_t st, const void* X, const void* W, in
 }
 
 static void linear_ln(bs_stage* s, hipStream_t st, const float* x, int row_stride, int row_offset, const void* g,
-                      const void* b, const void* W, int M, int N, int K, const Epi& ep, int out_bytes,
-                      const float* stats = nullptr) {
+                      const void* b, const void* W, int M, int N, int K, const Epi& ep, int out_bytes) {
   const bool decode = M <= 32 && s->bf16;
   if (decode) {
     ProfScope p(s, st, 1, gemv_bytes(s, M, N, K, out_bytes));
-    launch_linear_ln(s->bf16, x, row_stride, row_offset, g, b, s->d.ln_eps, s->xn, W, M, N, K, ep, st, stats);
+    launch_linear_ln(s->bf16, x, row_stride, row_offset, g, b, s->d.ln_eps, s->xn, W, M, N, K, ep, st);
   } else {
     ProfScope p(s, st, 2, 2.0 * M * N * K);
     launch_linear_ln(s->bf16, x, row_stride, row_offset, g, b, s->d.ln_eps, s->xn, W, M, N, K, ep, st);
   }
-}
-
-// The residual GEMV also publishes the LayerNorm statistics of its output rows into `stats` (Epi::ln_stats).
-static Epi with_ln_stats(const bs_stage* s, const Epi& ep, float* stats) {
-  Epi e = ep;
-  e.ln_stats = stats; e.ln_part = s->ln_part; e.ln_ticket = s->ln_ticket; e.ln_nblk = kLnBlocks; e.ln_eps = s->d.ln_eps;
-  return e;
 }
 
 // Algorithmic bytes of one int8 weight GEMV launch: int8 weights + row scales + bias + activations.
@@ -1029,9 +1008,9 @@ static void wlinear(bs_stage* s, hipStream_t st, const void* X, const Layer& w, 
 }
 
 static void wlinear_ln(bs_stage* s, hipStream_t st, const float* x, const void* g, const void* b, const Layer& w,
-                       int t, int M, int N, int K, const Epi& ep, int out_bytes, const float* stats = nullptr) {
+                       int t, int M, int N, int K, const Epi& ep, int out_bytes) {
   if (!w.sc[t]) {
-    linear_ln(s, st, x, 1, 0, g, b, w.t[t], M, N, K, ep, out_bytes, stats);
+    linear_ln(s, st, x, 1, 0, g, b, w.t[t], M, N, K, ep, out_bytes);
     return;
   }
   if (linear_q8_ln_fused(M, K)) {
@@ -1095,9 +1074,6 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
 
   // ---- decoder blocks
   const float inv_norm = 1.0f / std::sqrt((float)hd);
-  // batched decode: the dense / fc2 GEMVs publish their rows' LayerNorm statistics and LN_post + fc1 /
-  // the next LN_in + QKV (and ln_f + lm_head) normalise while staging them: no LayerNorm launch
-  const bool lnfuse = s->bf16 && !s->q8 && linear_ln_stats_supported(M, h);
   s->eng_used = 0;
   if (S == 1 && s->eng_ws && s->eng_on && engine_supported(d.device, M, h, nh, d.max_ctx)) {
     // every block in one persistent launch (engine.hip); the first stage gathers its embeddings there
@@ -1134,14 +1110,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
                                w.t[T_QKV_W], M, 3 * h, h, with_splitk(s, e), st);
       if (!done) launch_layernorm(s->bf16, s->wemb, ids, 0, 0, s->emb_g, s->emb_b, s->xa, 1, M, h, d.ln_eps, st);
     }
-    if (!done) {
-      // the first layer's input came over the hop (or from the embedding): its statistics in the units the
-      // fc2 GEMV publishes them in, so the layer normalises bit for bit as it would inside one stage
-      if (lnfuse && l == 0)
-        launch_ln_stats(cur, M, h, ln_stats_unit_cols(M, h, 4 * h), with_ln_stats(s, Epi{}, s->lnst[0]), st);
-      wlinear_ln(s, st, cur, w.t[T_LN1_G], w.t[T_LN1_B], w, T_QKV_W, M, 3 * h, h, with_splitk(s, e), 4,
-                 lnfuse ? s->lnst[0] : nullptr);
-    }
+    if (!done) wlinear_ln(s, st, cur, w.t[T_LN1_G], w.t[T_LN1_B], w, T_QKV_W, M, 3 * h, h, with_splitk(s, e), 4);
     // attention
     AttnArgs a{};
     a.q = s->q; a.k_cache = kbase; a.v_cache = kbase + s->kv_half; a.ctx_out = s->ctx; a.slopes = s->slopes;
@@ -1170,20 +1139,17 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
       if (w.sc[T_DENSE_W]) launch_linear_q8_parts(parts, (const int8_t*)w.t[T_DENSE_W], w.sc[T_DENSE_W], M, h, h, e2, st);
       else launch_linear_parts(parts, w.t[T_DENSE_W], M, h, h, e2, st);
     } else {
-      wlinear(s, st, s->ctx, w, T_DENSE_W, M, h, h, lnfuse ? with_ln_stats(s, with_splitk(s, e2), s->lnst[1])
-                                                          : with_splitk(s, e2), 4);
+      wlinear(s, st, s->ctx, w, T_DENSE_W, M, h, h, with_splitk(s, e2), 4);
     }
     // x2 = LN_post(a); g = gelu(x2 W1 + b1)
     Epi e3{};
     e3.kind = EPI_GELU; e3.bias = w.t[T_FC1_B]; e3.out_act = s->g; e3.ldo = 4 * h;
-    wlinear_ln(s, st, s->attn, w.t[T_LN2_G], w.t[T_LN2_B], w, T_FC1_W, M, 4 * h, h, with_splitk(s, e3), (int)s->esz,
-               lnfuse && !a.defer_merge ? s->lnst[1] : nullptr);
+    wlinear_ln(s, st, s->attn, w.t[T_LN2_G], w.t[T_LN2_B], w, T_FC1_W, M, 4 * h, h, with_splitk(s, e3), (int)s->esz);
     // x = a + g W2 + b2
     float* nxt = (!d.is_last && !host_io && l == s->L - 1) ? (float*)out : (cur == s->xa ? s->xb : s->xa);
     Epi e4{};
     e4.kind = EPI_RESID; e4.bias = w.t[T_FC2_B]; e4.out_f32 = nxt; e4.resid = s->attn; e4.ldo = h;
-    wlinear(s, st, s->g, w, T_FC2_W, M, h, 4 * h, lnfuse ? with_ln_stats(s, with_splitk(s, e4), s->lnst[0])
-                                                         : with_splitk(s, e4), 4);
+    wlinear(s, st, s->g, w, T_FC2_W, M, h, 4 * h, with_splitk(s, e4), 4);
     cur = nxt;
   }
 
@@ -1201,8 +1167,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
       e.logits = dev_logits;
     }
     if (sample && !e.logits) e.logits = s->sample_logits;
-    linear_ln(s, st, cur, S, S - 1, s->lnf_g, s->lnf_b, s->wemb, B, V, h, with_splitk(s, e), 0,
-              lnfuse && S == 1 && s->L > 0 ? s->lnst[0] : nullptr);
+    linear_ln(s, st, cur, S, S - 1, s->lnf_g, s->lnf_b, s->wemb, B, V, h, with_splitk(s, e), 0);
     int* tok_out = host_io ? s->tok : (int*)out;
     // the pick is the step's last kernel: it advances the device copy of every row's past_len by S
     if (sample)

@@ -56,12 +56,10 @@ def test_ldsw4_ragged_tile_columns(B):
 
 
 @pytest.mark.parametrize("B", [8, 32])
-def test_batched_decode_fused_layernorm_middle_stage(B):
-    """4 < B <= 32: the dense and fc2 GEMVs publish their output rows' LayerNorm statistics (per-block
-    (mean, M2) partials combined by the last arriver, Chan's update) and LN_post + fc1 / the next LN_in + QKV
-    normalise while staging them -- no ln_rows launch after the stage's first layer.  A 3-layer
-    bloom-1b1-width middle stage fed hidden states with a large common offset (|mean| 20 x std: a one-pass
-    sum-of-squares variance would cancel) decodes 3 steps; every output within the wide-block bound."""
+def test_batched_decode_middle_stage_offset_rows(B):
+    """4 < B <= 32 (ln_rows_kernel + gemv_ldsw4): a 3-layer bloom-1b1-width middle stage fed hidden states
+    with a large common offset (|mean| 20 x std: a plain one-pass sum-of-squares variance would cancel; the
+    kernel's shifted sums must not) decodes 3 steps; every output within the wide-block bound."""
     h, nh, L, V = 1536, 16, 4, 2048
     gs, os_ = pair(h, nh, L, V, 1, 4, "bf16", seed=31, max_batch=B, max_ctx=16, max_tokens=B * 4, is_first=False,
                    is_last=False)
@@ -73,6 +71,6 @@ def test_batched_decode_fused_layernorm_middle_stage(B):
         x1 = (20.0 + rng.standard_normal((B, 1, h))).astype(np.float32)
         yg = gs.forward_host(x1, B, 1, past_len=4 + step)
         yo = os_.forward(x1, B, 1, past_len=4 + step)
-        check_close(yg, yo, "bf16", f"B={B} fused-LN decode step {step}")
+        check_close(yg, yo, "bf16", f"B={B} offset-rows decode step {step}")
     gs.close()
     os_.close()
