@@ -136,6 +136,8 @@ struct bs_stage {
   float* sample_logits = nullptr;   // [max_batch][V] logits the sampler reads (device I/O without logits)
   // decode engine (engine.hip): workspace when the stage's shape allows it; on/off (bs_set_decode_engine)
   char* eng_ws = nullptr;
+  unsigned* eng_sticky = nullptr;   // host-mapped: 1 once an in-kernel wait of the engine expired (never reset)
+  unsigned* eng_sticky_dev = nullptr;
   size_t eng_layer_bytes = 0;
   int eng_on = 0;                   // bs_set_decode_engine (off until it beats the launches)
   int graphs_on = 1;                // bs_set_graphs: decode steps on device buffers replay captured graphs
@@ -251,6 +253,7 @@ static void free_stage(bs_stage* s) {
   if (s->sample_logits) hipFree(s->sample_logits);
   if (s->wtmp) hipFree(s->wtmp);
   if (s->eng_ws) hipFree(s->eng_ws);
+  if (s->eng_sticky) hipHostFree(s->eng_sticky);
   if (s->own) hipStreamDestroy(s->own);
   delete s;
 }
@@ -620,6 +623,10 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
     if (ok && hipMalloc((void**)&s->eng_ws, eb) == hipSuccess) {
       s->eng_layer_bytes = lb;
       HIP_TRY(hipMemsetAsync(s->eng_ws, 0, eb, s->own));
+      if (hipHostMalloc((void**)&s->eng_sticky, 4, hipHostMallocMapped) == hipSuccess) {
+        *s->eng_sticky = 0;
+        if (hipHostGetDevicePointer((void**)&s->eng_sticky_dev, s->eng_sticky, 0) != hipSuccess) s->eng_sticky_dev = nullptr;
+      }
     }
   }
   std::vector<float> sl(desc->n_head);
@@ -1087,6 +1094,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     ea.ids = ids; ea.wemb = s->wemb; ea.emb_g = s->emb_g; ea.emb_b = s->emb_b;
     ea.x_out = (!d.is_last && !host_io) ? (float*)out : (cur == s->xb ? s->xa : s->xb);
     ea.ws = s->eng_ws;
+    ea.sticky_host = s->eng_sticky_dev;
     double wbytes = (double)s->L * (12.0 * h * h + 13.0 * h) * 2.0;
     {
       ProfScope p(s, st, 1, wbytes + ctx_sum * nh * hd * 2 * s->esz + (double)M * h * 4 * 2);
@@ -1257,10 +1265,10 @@ extern "C" int bs_engine_status(bs_stage* s, int32_t* used, int32_t* status) {
   if (status) {
     *status = 0;
     if (s->eng_ws) {
-      // the last launch's timeout word (kept by the block that finished last)
+      // the sticky timeout word: set by any launch whose in-kernel wait expired, never reset
       uint32_t w = 0;
       HIP_TRY(hipMemcpy(&w, s->eng_ws + engine_status_offset(), 4, hipMemcpyDeviceToHost));
-      *status = (int32_t)w;
+      *status = (int32_t)(w | (s->eng_sticky ? *(volatile unsigned*)s->eng_sticky : 0u));
     }
   }
   return BS_OK;
@@ -1299,6 +1307,8 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
   }
   if (M > d.max_tokens) return fail(BS_ERR_INVALID, "batch*seq exceeds max_tokens");
   if (!in || !out) return fail(BS_ERR_INVALID, "in/out is NULL");
+  if (s->eng_sticky && *(volatile unsigned*)s->eng_sticky)
+    return fail(BS_ERR_DEVICE, "decode engine: an in-kernel wait expired in an earlier step (its outputs were garbage)");
   const bool want_logits = (step->flags & BS_STEP_LOGITS) != 0;
   if (want_logits && (!d.is_last || !logits)) return fail(BS_ERR_INVALID, "logits requested on a non-last stage or NULL");
   const bool host_io = (step->flags & BS_STEP_HOST_IO) != 0;
