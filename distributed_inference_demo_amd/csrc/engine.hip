@@ -132,9 +132,27 @@ template <int H> struct Smem {
   alignas(16) bf16 ctxh[C::HD];                       // attention merge: the head's context
   alignas(16) float res[32];                          // dot results of the phase's rows
   int landed, freed, dots_done, in_ready, att_ready, merge_ready, dead;
+#ifdef BS_ENGINE_STAMPS
+  unsigned long long stamps[24][16];                  // diagnostic builds: s_memrealtime per (layer, point)
+#endif
 };
 
 }  // namespace
+
+// Diagnostic builds only (tools/engine_timeline.hip defines BS_ENGINE_STAMPS): lane 0 of a wave records
+// s_memrealtime (100 MHz) at point k of layer l in LDS; the block copies them out at the end.  Points:
+// gather wave 0 x seen, 1 LN_in staged, 2 ctx seen, 3 x1 seen, 4 g seen; attention wave 5 q/k/v seen,
+// 6 record ready, 7 merged (split 0); publish wave 8 QKV dots done, 9 q/k/v published, 10 record published,
+// 11 ctx published (split 0), 12 x1 published, 13 g published, 14 x published; loader 15 layer issued.
+#ifdef BS_ENGINE_STAMPS
+__device__ unsigned long long g_eng_stamps[256 * 24 * 16];
+#define ESTAMP(l, k)                                                                                  \
+  do {                                                                                                \
+    if ((threadIdx.x & 63) == 0 && (l) < 24) sm->stamps[l][k] = __builtin_amdgcn_s_memrealtime();    \
+  } while (0)
+#else
+#define ESTAMP(l, k) do {} while (0)
+#endif
 
 typedef const __attribute__((address_space(4))) EngineArgs KArgs;  // kernarg segment: scalar loads
 __device__ __forceinline__ KArgs* kargs(uint64_t bits) {
@@ -252,6 +270,7 @@ __device__ __attribute__((noinline)) void role_loader(uint64_t ka) {
     // at most kD slots in flight: slot g - kD + 1 has landed once all but the youngest (kD - 1) * NC have
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kD - 1) * C::NC) : "memory");
     if (g >= kD - 1) lds_put(&sm->landed, g - kD + 2);
+    if (i == C::SL - 1) ESTAMP(l, 15);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_put(&sm->landed, total);
@@ -375,12 +394,15 @@ __device__ __attribute__((noinline)) void role_gather(uint64_t ka) {
           v[c][1] = v[c][1] * bf16_hi(g) + bf16_hi(be);
         }
       }
+      ESTAMP(l, 0);
       stage_ln(v, gb, eps);
       lds_put(&sm->in_ready, P0 + 1);
+      ESTAMP(l, 1);
     }
     phase_dots<H, 1>(a, sm, 0, l * C::SL + C::OQ, C::RQ, P0, sm->xa[0]);
     // ---- C: ctx -> xa[1]
     gather_bf16(WO::GCTX, H, tag_of(gen, L, l, E_CTX), sm->xa[1]);
+    ESTAMP(l, 2);
     lds_put(&sm->in_ready, P0 + 2);
     phase_dots<H, 1>(a, sm, 0, l * C::SL + C::OD, C::RD, P0 + 1, sm->xa[1]);
     // ---- D: x1 -> xf, LN_post -> xa[0]
@@ -389,12 +411,14 @@ __device__ __attribute__((noinline)) void role_gather(uint64_t ka) {
       load_gb((const bf16*)(wl + LO::LN2_G), (const bf16*)(wl + LO::LN2_B), gb);
       float v[NP][2];
       gather_f32(WO::GX1, tag_of(gen, L, l, E_X1), v);
+      ESTAMP(l, 3);
       stage_ln(v, gb, eps);
       lds_put(&sm->in_ready, P0 + 3);
     }
     phase_dots<H, 1>(a, sm, 0, l * C::SL + C::O1, C::R1, P0 + 2, sm->xa[0]);
     // ---- E: g -> xg
     gather_bf16(WO::GG, 4 * H, tag_of(gen, L, l, E_G), sm->xg);
+    ESTAMP(l, 4);
     lds_put(&sm->in_ready, P0 + 4);
     phase_dots<H, 4>(a, sm, 0, l * C::SL + C::O2, C::R2, P0 + 3, sm->xg);
   }
@@ -453,6 +477,7 @@ __device__ __attribute__((noinline)) void role_attn(uint64_t ka) {
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ESTAMP(l, 5);
     // scores: lane j <-> position p0 + j (ALiBi slope * position + q.k / sqrt(hd)), fp32 softmax partial
     {
       const int j = lane;
@@ -482,6 +507,7 @@ __device__ __attribute__((noinline)) void role_attn(uint64_t ka) {
       if (d1 < HD) sm->rec[2 + d1] = acc1;
       if (lane == 0) { sm->rec[0] = npos > 0 ? mx : -INFINITY; sm->rec[1] = lsum; }
       if (lane == 0) lds_put(&sm->att_ready, l + 1);
+      ESTAMP(l, 6);
     }
     if (s == 0) {
       // the head's 16 records -> ctx_h = sum_s w_s acc_s / sum_s w_s l_s, w_s = exp(m_s - max m)
@@ -516,6 +542,7 @@ __device__ __attribute__((noinline)) void role_attn(uint64_t ka) {
         }
       }
       if (lane == 0) lds_put(&sm->merge_ready, l + 1);
+      ESTAMP(l, 7);
     }
     phase_dots<H, 1>(a, sm, 1, l * C::SL + C::OD, C::RD, P0 + 1, sm->xa[1]);
     phase_dots<H, 1>(a, sm, 1, l * C::SL + C::O1, C::R1, P0 + 2, sm->xa[0]);
@@ -553,6 +580,7 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
     // ---- A: QKV rows -> q / k / v granules (this step's attention) and k, v to the cache (later steps)
     phase_dots<H, 1>(a, sm, 2, g0 + C::OQ, C::RQ, P0, sm->xa[0]);
     wait_ge<H>(a, sm, &sm->dots_done, 3 * (P0 + 1));
+    ESTAMP(l, 8);
     lds_put(&sm->freed, g0 + C::OD);
     if (lane < C::RQ / 2) {
       const float v0 = sm->res[jq] + bf16_lo(bq), v1 = sm->res[jq + 1] + bf16_hi(bq);
@@ -563,6 +591,7 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
       }
       put_granule(ws + WO::GQKV + (size_t)(nq / 2) * 8, tag_of(gen, L, l, E_QKV), pk);
     }
+    ESTAMP(l, 9);
     // ---- B: this split's record; the head's context (split 0)
     wait_ge<H>(a, sm, &sm->att_ready, l + 1);
     {
@@ -574,11 +603,13 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
         if (i < C::REC) put_granule(rec + i * 8, tp, __float_as_uint(sm->rec[i]));
       }
     }
+    ESTAMP(l, 10);
     if (s == 0) {
       wait_ge<H>(a, sm, &sm->merge_ready, l + 1);
       if (2 * lane < HD)
         put_granule(ws + WO::GCTX + (size_t)((head * HD) / 2 + lane) * 8, tag_of(gen, L, l, E_CTX),
                     pack_bf16x2((float)sm->ctxh[2 * lane], (float)sm->ctxh[2 * lane + 1]));
+      ESTAMP(l, 11);
     }
     // ---- C: dense -> x1 = x + dense(ctx) + bias
     phase_dots<H, 1>(a, sm, 2, g0 + C::OD, C::RD, P0 + 1, sm->xa[1]);
@@ -587,6 +618,7 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
     if (lane < C::RD)
       put_granule(ws + WO::GX1 + (size_t)nd * 8, tag_of(gen, L, l, E_X1),
                   __float_as_uint((sm->res[jd] + bf16_lo(bd)) + sm->xf[nd]));
+    ESTAMP(l, 12);
     // ---- D: fc1 + bias, GELU -> g
     phase_dots<H, 1>(a, sm, 2, g0 + C::O1, C::R1, P0 + 2, sm->xa[0]);
     wait_ge<H>(a, sm, &sm->dots_done, 3 * (P0 + 3));
@@ -594,6 +626,7 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
     if (lane < C::R1 / 2)
       put_granule(ws + WO::GG + (size_t)(n1 / 2) * 8, tag_of(gen, L, l, E_G),
                   pack_bf16x2(gelu_bloom(sm->res[j1] + bf16_lo(b1)), gelu_bloom(sm->res[j1 + 1] + bf16_hi(b1))));
+    ESTAMP(l, 13);
     // ---- E: fc2 -> x = x1 + fc2(g) + bias (the last layer writes the stage output)
     phase_dots<H, 4>(a, sm, 2, g0 + C::O2, C::R2, P0 + 3, sm->xg);
     wait_ge<H>(a, sm, &sm->dots_done, 3 * (P0 + 4));
@@ -603,6 +636,7 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
       if (l + 1 == L) a->x_out[n2] = y;
       else put_granule(ws + WO::GX + (size_t)n2 * 8, tag_of(gen, L, l, E_X), __float_as_uint(y));
     }
+    ESTAMP(l, 14);
   }
   // The block whose publisher finishes last advances the launch counter for the next launch's epochs.  Every
   // block has then published everything; its other waves may still be reading this launch's granules, which
@@ -632,6 +666,10 @@ __global__ __launch_bounds__(kThreads) void decode_engine_kernel(EngineArgs a) {
   else if (wv == 1) role_gather<H>(ka);
   else if (wv == 2) role_attn<H>(ka);
   else role_publish<H>(ka);
+#ifdef BS_ENGINE_STAMPS
+  __syncthreads();
+  for (int i = threadIdx.x; i < 24 * 16; i += kThreads) g_eng_stamps[(size_t)blockIdx.x * 24 * 16 + i] = (&sm->stamps[0][0])[i];
+#endif
 }
 
 // ------------------------------------------------------------------------------------

@@ -2477,8 +2477,8 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
     }
   };
   // The first tile is requested at the split's nominal start, clamped to the cache rather than to the
-  // context, so it does not wait for past_len: keys past the context are masked (p = 0) and the cache
-  // is zero-initialised and only ever holds finite values (0 * V stays 0).  An empty split drops it.
+  // context, so it does not wait for past_len: keys past the context are masked (p = 0) and their V is
+  // staged as 0 (below).  An empty split drops it.
   gload(nspl > 1 ? min(spl * a.pf_tiles * KT, a.max_ctx - 1) : 0, a.max_ctx - 1);
   for (int k0 = kbeg; k0 < kstop; k0 += KT) {
     __syncthreads();  // previous tile's LDS reads are done
@@ -2492,10 +2492,14 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
     }
     if (tid < nvi) {
       typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+      // keys past the split's end are staged as 0: their p is 0, but a stale cache row there (an earlier
+      // request's, past this one's context) could hold a value outside fp16's range, and 0 * inf is NaN
+      const int kv0 = k0 + vq * 4;
+      const bool ok0 = kv0 < kstop, ok1 = kv0 + 1 < kstop, ok2 = kv0 + 2 < kstop, ok3 = kv0 + 3 < kstop;
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        const f16x4 v4 = {(_Float16)(float)vreg[0][j], (_Float16)(float)vreg[1][j], (_Float16)(float)vreg[2][j],
-                          (_Float16)(float)vreg[3][j]};
+        const f16x4 v4 = {ok0 ? (_Float16)(float)vreg[0][j] : (_Float16)0.f, ok1 ? (_Float16)(float)vreg[1][j] : (_Float16)0.f,
+                          ok2 ? (_Float16)(float)vreg[2][j] : (_Float16)0.f, ok3 ? (_Float16)(float)vreg[3][j] : (_Float16)0.f};
         *reinterpret_cast<f16x4*>(&Vt[vsw(vdc + j, vq * 4)]) = v4;
       }
     }

@@ -1,10 +1,9 @@
 // tools/engine_timeline.hip — in-kernel timeline of the decode engine (diagnostic build, BS_ENGINE_STAMPS):
-// a bloom-1b1-shaped middle stage (24 layers, h 1536, 16 heads, B = 1, 580 cached positions, random
-// weights) launched back to back like graph replays; wave 0 of every block stamps s_memrealtime at five
-// points of each phase (start, input seen, S2 = activations staged, S3 = dots done, published; phase B:
-// start, q/k/v seen, attention done, split record published, head merged).
-// Prints per phase the median/p90 over blocks and layers of each segment, and per edge the latency from
-// the LAST producer's publish to the FIRST / median consumer's edge-seen stamp.
+// a bloom-1b1-shaped middle stage (24 layers, h 1536, 16 heads, B = 1, `past` cached positions, random
+// weights) launched back to back like graph replays; lane 0 of each role wave stamps s_memrealtime at the
+// points listed in engine.hip (ESTAMP).  Prints the launch time, per-phase segment medians over blocks and
+// layers, and per hand-off the latency from the LAST producer's publish to the median / last consumer's
+// "seen" stamp.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -DBS_ENGINE_STAMPS tools/engine_timeline.hip -o tools/engine_timeline
 #define BS_ENGINE_STAMPS 1
 #include "../distributed_inference_demo_amd/csrc/engine.hip"
@@ -34,7 +33,6 @@ int main(int argc, char** argv) {
   const size_t lb = engine_layer_bytes(H);
   char* w; CK(hipMalloc(&w, lb * L));
   fill_rand<<<4096, 256>>>((bf16*)w, lb * L / 2, 7, 0.04f);
-  // LayerNorm gammas near 1 (beta ~0): overwrite with 1.0 so the rows stay well scaled
   std::vector<bf16> ones(H, (bf16)1.0f);
   for (int l = 0; l < L; l++) {
     CK(hipMemcpy(w + l * lb + LayerOff<1536>::LN1_G, ones.data(), H * 2, hipMemcpyHostToDevice));
@@ -52,67 +50,83 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(slopes, hs.data(), NH * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(pastd, &past, 4, hipMemcpyHostToDevice));
   CK(hipDeviceSynchronize());
+  if (!engine_supported(0, 1, H, NH, MAXCTX)) { printf("engine not supported on this device\n"); return 1; }
   EngineArgs a{};
   a.wl = w; a.layer_stride = lb; a.kv = kv; a.kv_layer_stride = kvhalf * 2; a.kv_half = kvhalf;
   a.L = L; a.M = 1; a.h = H; a.n_head = NH; a.hd = HD; a.max_ctx = MAXCTX; a.slot = 0;
   a.eps = 1e-5f; a.inv_norm = 1.f / sqrtf((float)HD); a.slopes = slopes; a.past_dev = pastd;
-  a.x_in = xin; a.x_out = xout; a.ws = ws;
+  a.x_in = xin; a.x_out = xout; a.ws = ws; a.sticky_host = nullptr;
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int it = 0; it < 5; it++) launch_decode_engine(a, 0);
   const int iters = 20;
   CK(hipEventRecord(e0));
   for (int it = 0; it < iters; it++) launch_decode_engine(a, 0);
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-  printf("engine: %d back-to-back launches, %.1f us per launch (%.2f us per layer), past %d\n", iters, ms * 1e3 / iters,
-         ms * 1e3 / iters / L, past);
-  std::vector<unsigned long long> st((size_t)256 * 64 * 5 * 6);
+  unsigned sticky = 0;
+  CK(hipMemcpy(&sticky, ws + engine_status_offset(), 4, hipMemcpyDeviceToHost));
+  printf("engine: %d back-to-back launches, %.1f us per launch (%.2f us per layer), past %d, sticky %u\n", iters,
+         ms * 1e3 / iters, ms * 1e3 / iters / L, past, sticky);
+  std::vector<unsigned long long> st((size_t)256 * 24 * 16);
   CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_eng_stamps), st.size() * 8));
-  auto S = [&](int b, int l, int ph, int k) { return st[(((size_t)b * 64 + l) * 5 + ph) * 6 + k]; };
-  unsigned long long t0 = ~0ull, tend = 0;
-  for (int b = 0; b < 256; b++) { t0 = std::min(t0, S(b, 0, 0, 0)); tend = std::max(tend, S(b, L - 1, 4, 4)); }
-  printf("stamped span (first A start -> last E publish): %.2f us\n", (tend - t0) * 0.01);
-  const char* names[5] = {"A ln+qkv", "B attn", "C dense", "D ln+fc1", "E fc2"};
-  const char* seg[4] = {"wait", "stage", "dots", "publish"};
-  const char* segb[4] = {"wait", "attn", "record", "merge"};
-  for (int ph = 0; ph < 5; ph++) {
-    printf("%-9s", names[ph]);
-    for (int k = 0; k < 4; k++) {
-      std::vector<double> v;
-      for (int l = 1; l < L - 1; l++)
-        for (int b = 0; b < 256; b++) {
-          const unsigned long long x0 = S(b, l, ph, k), x1 = S(b, l, ph, k + 1);
-          if (x0 && x1 && x1 >= x0) v.push_back((x1 - x0) * 0.01);
-        }
-      printf(" | %-7s p50 %5.2f p90 %5.2f", ph == 1 ? segb[k] : seg[k], pct(v, .5), pct(v, .9));
-    }
-    printf("\n");
-  }
-  // per layer: span of each phase from the first block's start to the last block's publish
-  std::vector<double> layer_us;
-  for (int l = 1; l < L - 1; l++) {
-    unsigned long long a0 = ~0ull, a1 = 0;
-    for (int b = 0; b < 256; b++) { a0 = std::min(a0, S(b, l, 0, 0)); a1 = std::max(a1, S(b, l + 1, 0, 0)); }
-    layer_us.push_back((a1 - a0) * 0.01);
-  }
-  printf("layer (A start of first block -> next layer's last A start): p50 %.2f us\n", pct(layer_us, .5));
-  // edges: last publish of the producing phase -> consumers' edge-seen stamps
-  struct Edge { const char* n; int pph, cph, dl; } edges[] = {{"QKV->attn", 0, 1, 0}, {"X1->LN2", 2, 3, 0}, {"G->fc2", 3, 4, 0},
-                                                            {"X2->next A", 4, 0, 1}, {"CTX->dense", 1, 2, 0}};
-  for (auto& e : edges) {
-    std::vector<double> first, med, lastc;
-    for (int l = 1; l < L - 2; l++) {
-      unsigned long long lastp = 0;
-      for (int b = 0; b < 256; b++) lastp = std::max(lastp, S(b, l, e.pph, 4));
-      std::vector<double> c;
+  auto S = [&](int b, int l, int k) { return (double)st[((size_t)b * 24 + l) * 16 + k]; };
+  // segments inside a block (median over blocks and layers 1 .. L-2)
+  struct Seg { const char* n; int k0, k1; bool s0; } segs[] = {
+      {"A  LN_in (x seen -> staged)", 0, 1, false},   {"A  QKV dots (staged -> dots done)", 1, 8, false},
+      {"A  QKV publish (dots -> published)", 8, 9, false}, {"B  attention (qkv seen -> record)", 5, 6, false},
+      {"B  record publish (ready -> published)", 6, 10, false}, {"B  merge publish (merged -> ctx)", 7, 11, true},
+      {"C  dense (ctx seen -> x1 published)", 2, 12, false}, {"D  LN+fc1 (x1 seen -> g published)", 3, 13, false},
+      {"E  fc2 (g seen -> x published)", 4, 14, false}};
+  for (auto& sg : segs) {
+    std::vector<double> v;
+    for (int l = 1; l < L - 1; l++)
       for (int b = 0; b < 256; b++) {
-        const unsigned long long x = S(b, l + e.dl, e.cph, 1);
-        if (x) c.push_back(((double)x - (double)lastp) * 0.01);
+        if (sg.s0 && b % 16) continue;
+        const double x0 = S(b, l, sg.k0), x1 = S(b, l, sg.k1);
+        if (x0 > 0 && x1 >= x0) v.push_back((x1 - x0) * 0.01);
       }
-      if (c.empty()) continue;
-      first.push_back(pct(c, 0)); med.push_back(pct(c, .5)); lastc.push_back(pct(c, 1));
-    }
-    printf("edge %-11s last publish -> seen: first %.2f  median %.2f  last %.2f us\n", e.n, pct(first, .5), pct(med, .5),
-           pct(lastc, .5));
+    printf("%-42s p50 %6.2f p90 %6.2f us\n", sg.n, pct(v, .5), pct(v, .9));
   }
+  // hand-offs: last producer publish -> consumers' seen stamps (median over layers of per-layer median / max)
+  struct Edge { const char* n; int kp, kc, dl; int grp; } edges[] = {
+      {"x      (fc2 -> next LN_in)", 14, 0, 1, 0}, {"q/k/v  (QKV -> attention, head)", 9, 5, 0, 1},
+      {"record (attention -> merge, head)", 10, 7, 0, 2}, {"ctx    (merge -> dense)", 11, 2, 0, 0},
+      {"x1     (dense -> LN_post)", 12, 3, 0, 0}, {"g      (fc1 -> fc2)", 13, 4, 0, 0}};
+  for (auto& e : edges) {
+    std::vector<double> med, mx;
+    for (int l = 1; l < L - 2; l++) {
+      for (int hg = 0; hg < (e.grp ? 16 : 1); hg++) {
+        double lastp = 0;
+        for (int b = 0; b < 256; b++) {
+          if (e.grp && b / 16 != hg) continue;
+          if (e.kp == 11 && b % 16) continue;
+          lastp = std::max(lastp, S(b, l, e.kp));
+        }
+        std::vector<double> c;
+        for (int b = 0; b < 256; b++) {
+          if (e.grp && b / 16 != hg) continue;
+          if (e.grp == 2 && b % 16) continue;
+          const double x = S(b, l + e.dl, e.kc);
+          if (x > 0) c.push_back((x - lastp) * 0.01);
+        }
+        if (c.empty()) continue;
+        med.push_back(pct(c, .5));
+        mx.push_back(pct(c, 1));
+      }
+    }
+    printf("edge %-36s last publish -> seen: median %6.2f  last %6.2f us\n", e.n, pct(med, .5), pct(mx, .5));
+  }
+  // per layer: first block's x seen -> next layer's last block x seen
+  std::vector<double> lay;
+  for (int l = 1; l < L - 2; l++) {
+    double a0 = 1e30, a1 = 0;
+    for (int b = 0; b < 256; b++) { a0 = std::min(a0, S(b, l, 0)); a1 = std::max(a1, S(b, l + 1, 0)); }
+    lay.push_back((a1 - a0) * 0.01);
+  }
+  std::vector<double> ld;
+  for (int l = 1; l < L - 1; l++)
+    for (int b = 0; b < 256; b++) ld.push_back((S(b, l, 15) - S(b, l - 1, 15)) * 0.01);
+  printf("layer span p50 %.2f us; loader: layer issue interval p50 %.2f p90 %.2f us\n", pct(lay, .5), pct(ld, .5),
+         pct(ld, .9));
   return 0;
 }
