@@ -45,7 +45,16 @@
 namespace {
 
 constexpr int kG = 256, kThreads = 256, kNH = 16, kSplits = 16;
-constexpr int kD = 8;                                   // weight slots in flight per CU (loader)
+// Build knobs for tools/engine_timeline.hip's A/B binaries (the product library uses the defaults):
+// BS_ENGINE_D slots in flight per CU; BS_ENGINE_THIN = 1 holds the loader to one outstanding slot while the
+// CU's gather wave sweeps a hand-off (MI355X_MICROARCH.md "gather-pass").
+#ifndef BS_ENGINE_D
+#define BS_ENGINE_D 8
+#endif
+#ifndef BS_ENGINE_THIN
+#define BS_ENGINE_THIN 0
+#endif
+constexpr int kD = BS_ENGINE_D;                          // weight slots in flight per CU (loader)
 constexpr int kRingBytes = 96 * 1024;
 constexpr int kMaxPos = 64;                             // cached positions per attention split (contexts <= 1024)
 enum Edge { E_X = 0, E_QKV = 1, E_PART = 2, E_CTX = 3, E_X1 = 4, E_G = 5 };
@@ -131,7 +140,7 @@ template <int H> struct Smem {
   alignas(16) bf16 qkv[3][C::HD];                     // attention: the head's q, k, v of the new position
   alignas(16) bf16 ctxh[C::HD];                       // attention merge: the head's context
   alignas(16) float res[32];                          // dot results of the phase's rows
-  int landed, freed, dots_done, in_ready, att_ready, merge_ready, dead;
+  int landed, freed, dots_done, in_ready, att_ready, merge_ready, dead, gathering;
 #ifdef BS_ENGINE_STAMPS
   unsigned long long stamps[24][16];                  // diagnostic builds: s_memrealtime per (layer, point)
 #endif
@@ -260,6 +269,11 @@ __device__ __attribute__((noinline)) void role_loader(uint64_t ka) {
       }
       if (lds_get(&sm->dead)) break;
     }
+    if (BS_ENGINE_THIN && lds_get(&sm->gathering)) {
+      // the gather wave is sweeping: keep one slot in flight so its loads do not queue behind a burst
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_put(&sm->landed, g);
+    }
     const int l = g / C::SL, i = g - l * C::SL;
     const __amdgpu_buffer_rsrc_t r = rsrc(a->wl + (size_t)l * ls);
     const uint32_t so = src(i);
@@ -319,7 +333,9 @@ __device__ __attribute__((noinline)) void role_gather(uint64_t ka) {
   // fp32 granule vector (x, x1): v[c] = elements (c * 64 + lane) * 2 + {0, 1}
   auto gather_f32 = [&](size_t off, uint32_t tag, float (&v)[NP][2]) {
     uint32_t raw[NP][2];
+    if (BS_ENGINE_THIN) lds_put(&sm->gathering, 1);
     sweep<H, NP>(a, sm, rsrc(a->ws + off), H / 2, [&](int p) { return (uint32_t)(p * 16); }, tag, raw);
+    if (BS_ENGINE_THIN) lds_put(&sm->gathering, 0);
 #pragma unroll
     for (int c = 0; c < NP; c++) { v[c][0] = __uint_as_float(raw[c][0]); v[c][1] = __uint_as_float(raw[c][1]); }
   };
@@ -328,7 +344,9 @@ __device__ __attribute__((noinline)) void role_gather(uint64_t ka) {
     constexpr int NCB = H / 64;  // loads per lane for n = 4H
     uint32_t raw[NCB][2];
     const int np = n / 4;
+    if (BS_ENGINE_THIN) lds_put(&sm->gathering, 1);
     sweep<H, NCB>(a, sm, rsrc(a->ws + off), np, [&](int p) { return (uint32_t)(p * 16); }, tag, raw);
+    if (BS_ENGINE_THIN) lds_put(&sm->gathering, 0);
 #pragma unroll
     for (int c = 0; c < NCB; c++) {
       const int p = c * 64 + lane;
@@ -657,7 +675,7 @@ __global__ __launch_bounds__(kThreads) void decode_engine_kernel(EngineArgs a) {
   Smem<H>* sm = smem<H>();
   if (threadIdx.x == 0) {
     sm->landed = 0; sm->freed = 0; sm->dots_done = 0; sm->in_ready = 0; sm->att_ready = 0; sm->merge_ready = 0;
-    sm->dead = 0;
+    sm->dead = 0; sm->gathering = 0;
   }
   __syncthreads();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
