@@ -1078,7 +1078,9 @@ __device__ __forceinline__ bf16x8 q8x8_to_bf16(const uint2 raw) {
 
 // WT = bf16 (KC = 64 columns = 128 B per row per stage) or int8_t (KC = 128 columns = 128 B; each A fragment
 // is 8 bytes converted in registers, the row scale applied by the epilogue's col_scale).
-template <int T, int WAVES, int MT, typename WT = bf16>
+// PD: stages in flight per wave (register ring): 2, or 3 when a wave's K part is exactly 3 stages (the
+// bloom-1b1 widths), so every load of the wave is issued before its first stage waits.
+template <int T, int WAVES, int MT, typename WT = bf16, int PD = 2>
 __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __restrict__ W, const bf16* __restrict__ X,
                                                                int M, int N, int K, Epi ep) {
   constexpr int RB = 128, KC = RB / (int)sizeof(WT);  // bytes / columns of one row per stage
@@ -1102,8 +1104,8 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
   const bf16* xsrc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; mt++) xsrc[mt] = X + (size_t)min(mt * 16 + r, M - 1) * K + kbeg + g * 8;
-  u32x4v wr[2][NI];
-  bf16x8 xr[2][MT][KSTEP];
+  u32x4v wr[PD][NI];
+  bf16x8 xr[PD][MT][KSTEP];
   auto load = [&](int st, u32x4v (&ww)[NI], bf16x8 (&xx)[MT][KSTEP]) {
     const size_t o = (size_t)st * KC;
 #pragma unroll
@@ -1122,7 +1124,8 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
 #pragma unroll
     for (int mt = 0; mt < MT; mt++) acc[t][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   auto stage = [&](int b, int st) {
-    if (st + 1 < nst) load(st + 1, wr[b ^ 1], xr[b ^ 1]);
+    const int nb = (b + PD - 1) % PD;  // the ring slot of stage st + PD - 1
+    if (st + PD - 1 < nst) load(st + PD - 1, wr[nb], xr[nb]);
 #pragma unroll
     for (int i = 0; i < NI; i++) *reinterpret_cast<u32x4v*>(&wl[swz(RPI * i + lr, lc * 16)]) = wr[b][i];
     __builtin_amdgcn_wave_barrier();
@@ -1140,10 +1143,13 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
     __builtin_amdgcn_wave_barrier();
   };
   if (nst > 0) {
-    load(0, wr[0], xr[0]);
-    for (int st = 0; st < nst; st += 2) {
-      stage(0, st);
-      if (st + 1 < nst) stage(1, st + 1);
+#pragma unroll
+    for (int p = 0; p < PD - 1; p++)
+      if (p < nst) load(p, wr[p], xr[p]);
+    for (int st = 0; st < nst; st += PD) {
+#pragma unroll
+      for (int p = 0; p < PD; p++)
+        if (st + p < nst) stage(p, st + p);
     }
   }
   tiles_epilogue<T, MT, WAVES>(acc, red, M, N, n0, ep);
@@ -1153,7 +1159,14 @@ template <int T, int WAVES, int MT, typename WT>
 static void gemv_ldsw4_launch(const bf16* X, const WT* W, int M, int N, int K, int KS, const Epi& ep, hipStream_t s) {
   const size_t shm = (size_t)WAVES * T * 16 * 128 + sizeof(float) * WAVES * (T * 16) * (MT * 16 + 1);
   const int blocks = (N + T * 16 - 1) / (T * 16);
-  gemv_ldsw4_kernel<T, WAVES, MT, WT><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+  constexpr int KC = 128 / (int)sizeof(WT);
+  if constexpr (sizeof(WT) == 2) {
+    if (K / (KS * WAVES * KC) == 3) {
+      gemv_ldsw4_kernel<T, WAVES, MT, WT, 3><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+      return;
+    }
+  }
+  gemv_ldsw4_kernel<T, WAVES, MT, WT, 2><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
 }
 
 template <int T, int MT, int WAVES, typename WT = bf16>
