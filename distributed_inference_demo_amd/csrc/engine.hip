@@ -94,6 +94,13 @@ __device__ __forceinline__ void lds_put(int* p, int v) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS data writes land before the flag
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// The loader's publish of `landed`: an inline-asm ds_write, which the compiler does not see as an LDS access
+// -- for a visible one it drains the wave's LDS-DMA first (vmcnt(0): it cannot tell the ring from the word),
+// which held the loader to one slot in flight (4 GB/s per CU, round-4 first timeline).  The explicit counted
+// vmcnt before it is what orders the landed slots.
+__device__ __forceinline__ void lds_put_loader(uint32_t off, int v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v));
+}
 __device__ __forceinline__ void lds_add(int* p, int v) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -254,6 +261,12 @@ __device__ __attribute__((noinline)) void role_loader(uint64_t ka) {
     else o = LO::FC2_W + (size_t)b * C::R2 * 4 * C::SLOT + (size_t)(i - C::O2) * C::SLOT;
     return (uint32_t)o + lane * 16;
   };
+  // Everything the steady loop needs lives in registers: the asm waits below clobber "memory", which would
+  // otherwise re-load the LDS base (a table lookup in a non-kernel function) and the kernel arguments per slot.
+  uint32_t ring0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)sm->ring;
+  uint32_t landed_off = (uint32_t)(size_t)(__attribute__((address_space(3))) int*)&sm->landed;
+  const char* wl0 = a->wl;
+  asm volatile("" : "+s"(ring0), "+s"(landed_off), "+s"(wl0));  // opaque: held, not re-derived per slot
   int freed = 0;
   for (int g = 0; g < total; g++) {
     if (g - freed >= C::NS) {
@@ -271,20 +284,26 @@ __device__ __attribute__((noinline)) void role_loader(uint64_t ka) {
     }
     if (BS_ENGINE_THIN && lds_get(&sm->gathering)) {
       // the gather wave is sweeping: keep one slot in flight so its loads do not queue behind a burst
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (the visible LDS read above already drained the DMA: the thinning this build measures)
       lds_put(&sm->landed, g);
     }
     const int l = g / C::SL, i = g - l * C::SL;
-    const __amdgpu_buffer_rsrc_t r = rsrc(a->wl + (size_t)l * ls);
+    const __amdgpu_buffer_rsrc_t r = rsrc(wl0 + (size_t)l * ls);
     const uint32_t so = src(i);
-    char* dst = sm->ring + (g % C::NS) * C::SLOT;
+    const uint32_t dst = ring0 + (uint32_t)((g % C::NS) * C::SLOT);
 #pragma unroll
     for (int p = 0; p < C::NC; p++)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(dst + p * 1024), 16, so + p * 1024, 0, 0, 2 /* nt */);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(size_t)(dst + p * 1024), 16, so + p * 1024, 0, 0, 2 /* nt */);
     // at most kD slots in flight: slot g - kD + 1 has landed once all but the youngest (kD - 1) * NC have
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kD - 1) * C::NC) : "memory");
-    if (g >= kD - 1) lds_put(&sm->landed, g - kD + 2);
-    if (i == C::SL - 1) ESTAMP(l, 15);
+    if (g >= kD - 1) lds_put_loader(landed_off, g - kD + 2);
+#ifdef BS_ENGINE_STAMPS
+    if (i == C::SL - 1 && l < 24 && lane == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      asm volatile("ds_write_b64 %0, %1" ::"v"(landed_off + (uint32_t)((char*)&sm->stamps[l][15] - (char*)&sm->landed)),
+                   "v"(t));
+    }
+#endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_put(&sm->landed, total);
