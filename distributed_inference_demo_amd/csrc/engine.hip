@@ -13,13 +13,14 @@
 // (2-4 us per edge, 32.8 us per layer: profiles/r03_engine_timeline.txt).  Per workgroup (256 threads):
 //   wave 0  LOADER: the only wave that streams weights -- LDS-DMA (buffer_load ... lds, nt) of the block's rows
 //           of every layer, in use order, into a ring of NS slots (one slot = one 2H-byte weight row of QKV /
-//           dense / fc1, a quarter row of fc2); at most D slots in flight; `landed` / `freed` words in LDS.
+//           dense / fc1, a quarter row of fc2); at most D slots in flight; `landed` in LDS; a slot is free once
+//           every dot wave has moved past its row (per-wave `need` words: the ring refills row by row).
 //   wave 1  GATHER: every all-to-all hand-off (x, ctx, x1, g: granule sweeps) and the LayerNorms; stages each
 //           phase's input vector in LDS.
-//   wave 2  ATTENTION: the block's (head, context split): cached K/V rows requested at the layer's start, the
-//           head's new q/k/v gathered, one (max, sum, acc) record; the head's split-0 block merges the 16
-//           records into ctx.
-//   wave 3  PUBLISH: every epilogue (bias, residual, GELU, KV-cache row) and every global store; frees slots.
+//   wave 2  ATTENTION: the block's (head, context split): the head's new q/k/v gathered, the split's cached K/V
+//           rows (landed in LDS by the loader), one (max, sum, acc) record from three partials (waves 2, 1, 3 each
+//           take a third of the rows); the head's split-0 block merges the 16 records into ctx.
+//   wave 3  PUBLISH: every epilogue (bias, residual, GELU, KV-cache row) and every global store.
 //   Dot products of every phase: rows split over waves 1-3 (v_dot2 on LDS weights x registered activations).
 // Loads and stores live on different waves: a wave with write-through stores pending would wait for them
 // before using any later load (the compiler's vmcnt is in order).
@@ -46,7 +47,7 @@ namespace {
 
 constexpr int kG = 256, kThreads = 256, kNH = 16, kSplits = 16;
 // Build knobs for tools/engine_timeline.hip's A/B binaries (the product library uses the defaults):
-// BS_ENGINE_D slots in flight per CU; BS_ENGINE_THIN = 1 holds the loader to one outstanding slot while the
+// BS_ENGINE_D slots in flight per CU; BS_ENGINE_THIN = T > 0 holds the loader to T outstanding slots while the
 // CU's gather wave sweeps a hand-off (MI355X_MICROARCH.md "gather-pass").
 #ifndef BS_ENGINE_D
 #define BS_ENGINE_D 8
@@ -55,7 +56,6 @@ constexpr int kG = 256, kThreads = 256, kNH = 16, kSplits = 16;
 #define BS_ENGINE_THIN 0
 #endif
 constexpr int kD = BS_ENGINE_D;                          // weight slots in flight per CU (loader)
-constexpr int kRingBytes = 96 * 1024;
 constexpr int kMaxPos = 64;                             // cached positions per attention split (contexts <= 1024)
 enum Edge { E_X = 0, E_QKV = 1, E_PART = 2, E_CTX = 3, E_X1 = 4, E_G = 5 };
 constexpr unsigned long long kSpinTicks = 20000000ull;  // 200 ms of s_memrealtime (100 MHz)
@@ -78,9 +78,10 @@ __device__ __forceinline__ void put_granule(void* p, uint32_t tag, uint32_t valu
 __device__ __forceinline__ uint32_t tag_of(uint32_t gen, int L, int l, int e) {
   return 0x80000000u | (((gen * (uint32_t)L + (uint32_t)l) * 8u + (uint32_t)e) & 0x7FFFFFFFu);
 }
-__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  const bf16 x = (bf16)a, y = (bf16)b;
-  return (uint32_t)__builtin_bit_cast(unsigned short, x) | ((uint32_t)__builtin_bit_cast(unsigned short, y) << 16);
+typedef float f2v __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_add / v_pk_mul / v_pk_fma_f32)
+typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2v{a, b}, bf2v));
 }
 __device__ __forceinline__ float bf16_lo(uint32_t v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t v) { return __uint_as_float(v & 0xFFFF0000u); }
@@ -100,6 +101,13 @@ __device__ __forceinline__ void lds_put(int* p, int v) {
 // vmcnt before it is what orders the landed slots.
 __device__ __forceinline__ void lds_put_loader(uint32_t off, int v) {
   asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v));
+}
+// An LDS word read the compiler does not see either (the loader polls att_ready with it between LDS-DMA
+// issues without draining them).
+__device__ __forceinline__ int lds_peek_loader(uint32_t off) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(off));
+  return __builtin_amdgcn_readfirstlane(v);
 }
 __device__ __forceinline__ void lds_add(int* p, int v) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -121,7 +129,8 @@ template <int H> struct Cfg {
   static constexpr int RQ = 3 * H / kG, RD = H / kG, R1 = 4 * H / kG, R2 = H / kG;  // rows per block
   static constexpr int SQ = RQ, SD = RD, S1 = R1, S2 = 4 * R2;       // ring slots per phase (slot = 2H bytes)
   static constexpr int OQ = 0, OD = SQ, O1 = SQ + SD, O2 = SQ + SD + S1, SL = SQ + SD + S1 + S2;
-  static constexpr int SLOT = 2 * H, NS = kRingBytes / SLOT;
+  // ring slots: what the 160 KB of LDS holds beside the rest of Smem (with the diagnostic stamps)
+  static constexpr int SLOT = 2 * H, NS = H == 1536 ? 35 : 60, RING = NS * SLOT;
   static_assert(NS >= S1 && NS >= S2 && NS >= SQ, "a phase's slots fit the ring");
   static_assert(kD * NC <= 63, "vmcnt immediate");
 };
@@ -136,22 +145,26 @@ template <int H> struct WsOff {
 
 template <int H> struct Smem {
   using C = Cfg<H>;
-  alignas(16) char ring[kRingBytes];                  // weight slots (LDS-DMA destination)
+  alignas(16) char ring[C::RING];                     // weight slots (LDS-DMA destination)
   alignas(16) bf16 xa[2][H];                          // phase inputs: LN_in out / ctx (A, C: 0 / 1), LN_post out (D: 0)
   alignas(16) bf16 xg[4 * H];                         // phase E input: g
-  alignas(16) float xf[H];                            // residual rows: x during A..C, x1 during D..E
+  alignas(16) float xf[C::RD];                        // the block's residual rows (dense = fc2 rows): x during A..C, x1 during D..E
   alignas(16) bf16 kv[2][kMaxPos][C::HD];             // attention: this split's cached K and V rows
-  alignas(16) float mg[kSplits][C::REC];              // attention merge (split 0): the head's records
+  alignas(16) float mg[kSplits][C::REC];              // attention: the 3 partials, then the merge (split 0): the head's records
   alignas(16) float pr[kMaxPos];                      // attention: probabilities
   alignas(16) float rec[C::REC];                      // attention: this split's record
   alignas(16) bf16 qkv[3][C::HD];                     // attention: the head's q, k, v of the new position
   alignas(16) bf16 ctxh[C::HD];                       // attention merge: the head's context
   alignas(16) float res[32];                          // dot results of the phase's rows
-  int landed, freed, dots_done, in_ready, att_ready, merge_ready, dead, gathering;
+  int landed, dots_done, in_ready, att_ready, merge_ready, dead, gathering, qkv_ready, att_parts;
+  int need[3];                                        // per dot wave: the first slot it may still read
 #ifdef BS_ENGINE_STAMPS
   unsigned long long stamps[24][16];                  // diagnostic builds: s_memrealtime per (layer, point)
 #endif
 };
+
+static_assert(sizeof(Smem<1536>) <= 163840 && sizeof(Smem<1024>) <= 163840, "one workgroup's LDS");
+static_assert(Cfg<1536>::RD == Cfg<1536>::R2 && Cfg<1024>::RD == Cfg<1024>::R2, "xf holds the dense = fc2 rows");
 
 }  // namespace
 
@@ -227,19 +240,26 @@ __device__ void sweep(KArgs* a, Smem<H>* sm, __amdgpu_buffer_rsrc_t r, int npair
 // pairs each lane holds (elements (c * 64 + lane) * 2 + {0, 1}).
 template <int NP>
 __device__ __forceinline__ void ln_pairs(float (&v)[NP][2], float eps, int n) {
-  float s = 0.f;
+  // one wave does a whole row: packed fp32 halves its VALU issue (the LayerNorm is issue-bound, ~4 cycles
+  // per wave64 instruction)
+  f2v s = {0.f, 0.f};
 #pragma unroll
-  for (int c = 0; c < NP; c++) s += v[c][0] + v[c][1];
-  const float mean = wave_sum(s) / (float)n;
-  float q = 0.f;
+  for (int c = 0; c < NP; c++) s += f2v{v[c][0], v[c][1]};
+  const float mean = wave_sum(s.x + s.y) / (float)n;
+  const f2v m2 = {mean, mean};
+  f2v q = {0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < NP; c++) {
-    const float d0 = v[c][0] - mean, d1 = v[c][1] - mean;
-    q += d0 * d0 + d1 * d1;
+    const f2v d = f2v{v[c][0], v[c][1]} - m2;
+    q = __builtin_elementwise_fma(d, d, q);
   }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)n + eps);
+  const float rstd = 1.0f / sqrtf(wave_sum(q.x + q.y) / (float)n + eps);
+  const f2v r2 = {rstd, rstd};
 #pragma unroll
-  for (int c = 0; c < NP; c++) { v[c][0] = (v[c][0] - mean) * rstd; v[c][1] = (v[c][1] - mean) * rstd; }
+  for (int c = 0; c < NP; c++) {
+    const f2v t = (f2v{v[c][0], v[c][1]} - m2) * r2;
+    v[c][0] = t.x; v[c][1] = t.y;
+  }
 }
 
 // ============ wave 0: the weight loader
@@ -265,29 +285,66 @@ __device__ __attribute__((noinline)) void role_loader(uint64_t ka) {
   // otherwise re-load the LDS base (a table lookup in a non-kernel function) and the kernel arguments per slot.
   uint32_t ring0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)sm->ring;
   uint32_t landed_off = (uint32_t)(size_t)(__attribute__((address_space(3))) int*)&sm->landed;
+  uint32_t att_off = (uint32_t)(size_t)(__attribute__((address_space(3))) int*)&sm->att_ready;
+  uint32_t kv_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)&sm->kv[0][0][0];
   const char* wl0 = a->wl;
-  asm volatile("" : "+s"(ring0), "+s"(landed_off), "+s"(wl0));  // opaque: held, not re-derived per slot
+  // this block's attention split (wave 2's head and positions): its cached K / V rows are contiguous
+  // [ncache][HD] in the cache and land in sm->kv by LDS-DMA ahead of each layer's QKV slots
+  constexpr int HD = C::HD, NKV = kMaxPos * HD * 2 / 1024;
+  const int head = b / kSplits, s = b % kSplits, past = a->past_dev[0];
+  const int per = (past + 1 + kSplits - 1) / kSplits, p0 = s * per;
+  const int ncache = max(0, min(p0 + per, past) - p0);
+  const int kvbytes = ncache * HD * 2;
+  const char* kv0 = a->kv + ((size_t)a->slot * kNH + head) * a->max_ctx * HD * 2 + (size_t)(ncache > 0 ? p0 : 0) * HD * 2;
+  uint32_t gath_off = (uint32_t)(size_t)(__attribute__((address_space(3))) int*)&sm->gathering;
+  asm volatile("" : "+s"(ring0), "+s"(landed_off), "+s"(att_off), "+s"(kv_lds), "+s"(wl0), "+s"(kv0), "+s"(gath_off));
+  int pub = 0;  // landed as published: monotone (the ring-full and thinned paths publish ahead of the counted one)
+  auto publish = [&](int v) {
+    if (v > pub) { pub = v; lds_put_loader(landed_off, v); }
+  };
   int freed = 0;
   for (int g = 0; g < total; g++) {
     if (g - freed >= C::NS) {
       // the ring is full: everything issued lands first (consumers may be waiting for it), then wait for room
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_put(&sm->landed, g);
+      publish(g);
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
-        freed = lds_get(&sm->freed);
+        freed = min(lds_get(&sm->need[0]), min(lds_get(&sm->need[1]), lds_get(&sm->need[2])));
         if (g - freed < C::NS || lds_get(&sm->dead)) break;
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) { expire<H>(a, sm); break; }
       }
       if (lds_get(&sm->dead)) break;
     }
-    if (BS_ENGINE_THIN && lds_get(&sm->gathering)) {
-      // the gather wave is sweeping: keep one slot in flight so its loads do not queue behind a burst
-      // (the visible LDS read above already drained the DMA: the thinning this build measures)
-      lds_put(&sm->landed, g);
+    if (BS_ENGINE_THIN && lds_peek_loader(gath_off)) {
+      // the gather wave is sweeping: at most BS_ENGINE_THIN slots in flight (this one included), so its loads
+      // do not queue behind a refill burst (MI355X_MICROARCH.md "gather-pass")
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((BS_ENGINE_THIN - 1) * C::NC) : "memory");
+      publish(g - BS_ENGINE_THIN + 1);
     }
     const int l = g / C::SL, i = g - l * C::SL;
+    if (i == 0 && kvbytes > 0) {
+      // layer l's K / V rows of the split, once the attention wave is done with layer l - 1's; loads return
+      // in order, so they have landed once slot g + 1 has (the attention wave's first QKV row waits for it)
+      if (l > 0 && lds_peek_loader(att_off) < l) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (lds_peek_loader(att_off) < l) {
+          if (lds_get(&sm->dead)) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) { expire<H>(a, sm); break; }
+        }
+      }
+      const char* kl = kv0 + (size_t)l * a->kv_layer_stride;
+      const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(kl), (short)0, kvbytes, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(kl + a->kv_half), (short)0, kvbytes, 0x00020000);
+#pragma unroll
+      for (int c = 0; c < NKV; c++) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void*)(size_t)(kv_lds + c * 1024), 16, c * 1024 + lane * 16, 0, 0, 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void*)(size_t)(kv_lds + kMaxPos * HD * 2 + c * 1024), 16,
+                                                 c * 1024 + lane * 16, 0, 0, 2);
+      }
+    }
     const __amdgpu_buffer_rsrc_t r = rsrc(wl0 + (size_t)l * ls);
     const uint32_t so = src(i);
     const uint32_t dst = ring0 + (uint32_t)((g % C::NS) * C::SLOT);
@@ -296,7 +353,7 @@ __device__ __attribute__((noinline)) void role_loader(uint64_t ka) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(size_t)(dst + p * 1024), 16, so + p * 1024, 0, 0, 2 /* nt */);
     // at most kD slots in flight: slot g - kD + 1 has landed once all but the youngest (kD - 1) * NC have
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kD - 1) * C::NC) : "memory");
-    if (g >= kD - 1) lds_put_loader(landed_off, g - kD + 2);
+    publish(g - kD + 2);
 #ifdef BS_ENGINE_STAMPS
     if (i == C::SL - 1 && l < 24 && lane == 0) {
       const unsigned long long t = __builtin_amdgcn_s_memrealtime();
@@ -331,9 +388,103 @@ __device__ __forceinline__ void phase_dots(KArgs* a, Smem<H>* sm, int wc, int g0
       acc = dot8(w, xr[c], acc);
     }
     const float v = wave_sum(acc);
-    if (lane == 0) sm->res[j] = v;
+    if (lane == 0) {
+      sm->res[j] = v;
+      // this wave's next row (or the phase end): every slot before it is read -- the loader may refill it
+      lds_put(&sm->need[wc], g0 + min(j + 3, nrows) * SPR);
+    }
   }
   if (lane == 0) lds_add(&sm->dots_done, 1);
+}
+
+// ============ one third of the split's attention: rows j of passes [q pp, (q + 1) pp) (4 rows per pass, 16 lanes
+// per row, 8 dims each -- every LDS read a contiguous 16-B chunk of one row) -> the partial (max, sum, acc) in
+// mg[q] (the merge area is free until the record edge).  Waves 2, 1 and 3 take parts 0, 1, 2: the attention is
+// issue-bound on one wave (~4 cycles per wave64 instruction), and waves 1 and 3 would otherwise wait.
+// Row j < ncache is a cached row (sm->kv), j == ncache (position `past`) the new k / v, rows past npos masked.
+template <int H>
+__device__ __forceinline__ void attn_part(Smem<H>* sm, int q, int p0, int npos, int ncache, float slope, float inv_norm) {
+  using C = Cfg<H>;
+  constexpr int HD = C::HD, NSL = HD / 8;
+  const int lane = threadIdx.x & 63, grp = lane >> 4, ds = lane & 15;
+  const bool dv = ds < NSL;
+  const int doff = dv ? ds * 8 : 0;
+  const int npass = (npos + 3) / 4, pp = (npass + 2) / 3;  // passes <= kMaxPos / 4
+  const int t0 = min(q * pp, npass), t1 = min(t0 + pp, npass);
+  const bf16x8 q8 = *reinterpret_cast<const bf16x8*>(sm->qkv[0] + doff);
+  float mx = -INFINITY;
+  for (int t = t0; t < t1; t += 4) {
+    bf16x8 kk[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int j = min((t + u) * 4 + grp, kMaxPos - 1);
+      kk[u] = *reinterpret_cast<const bf16x8*>((j < ncache ? sm->kv[0][j] : sm->qkv[1]) + doff);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int j = (t + u) * 4 + grp;
+      float d = dot8(kk[u], q8, 0.f);
+      d = dv ? d : 0.f;
+      d += dpp_f<0xB1>(d);   // sum over the row's 16 lanes: xor 1, xor 2, rotate 4, rotate 8
+      d += dpp_f<0x4E>(d);
+      d += dpp_f<0x124>(d);
+      d += dpp_f<0x128>(d);
+      const bool mine = t + u < t1;
+      const float sc = mine && j < npos ? slope * (float)(p0 + j) + inv_norm * d : -INFINITY;
+      if (ds == 0 && mine) sm->pr[j] = sc;
+      mx = fmaxf(mx, sc);
+    }
+  }
+  mx = wave_max(mx);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // fp32 softmax partial: lane i <-> row 4 t0 + i
+  const int jr = 4 * t0 + lane;
+  const bool own = lane < 4 * (t1 - t0) && jr < npos;
+  const float e = own ? __expf(sm->pr[min(jr, kMaxPos - 1)] - mx) : 0.f;
+  const float lsum = wave_sum(e);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (own) sm->pr[jr] = e;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) acc[k] = 0.f;
+  for (int t = t0; t < t1; t += 4) {
+    bf16x8 vv[4];
+    float pj[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int j = min((t + u) * 4 + grp, kMaxPos - 1);
+      vv[u] = *reinterpret_cast<const bf16x8*>((j < ncache ? sm->kv[1][j] : sm->qkv[2]) + doff);
+      pj[u] = sm->pr[j];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int j = (t + u) * 4 + grp;
+      const float w = t + u < t1 && j < npos ? pj[u] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; k++) acc[k] += w * (float)vv[u][k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    acc[k] += __shfl_xor(acc[k], 16, 64);
+    acc[k] += __shfl_xor(acc[k], 32, 64);
+  }
+  if (grp == 0 && dv) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) sm->mg[q][2 + doff + k] = acc[k];
+  }
+  if (lane == 0) { sm->mg[q][0] = mx; sm->mg[q][1] = lsum; }
+}
+
+// The block's attention split: positions [p0, p0 + npos), ncache of them cached.
+__device__ __forceinline__ void attn_split(KArgs* a, int b, int& p0, int& npos, int& ncache) {
+  const int past = a->past_dev[0], s = b % kSplits;
+  const int per = (past + 1 + kSplits - 1) / kSplits;  // positions per split (<= kMaxPos)
+  p0 = s * per;
+  const int p1 = min(p0 + per, past + 1);
+  ncache = max(0, min(p1, past) - p0);
+  npos = max(0, p1 - p0);
 }
 
 // ============ wave 1: the all-to-all gathers and the LayerNorms; stages each phase's input
@@ -349,6 +500,10 @@ __device__ __attribute__((noinline)) void role_gather(uint64_t ka) {
   const int L = a->L;
   const size_t ls = a->layer_stride;
   const uint32_t gen = __builtin_amdgcn_readfirstlane(((const unsigned*)a->ws)[Ctl::GEN]);
+  int ap0, anpos, ancache;
+  attn_split(a, blockIdx.x, ap0, anpos, ancache);
+  float aslope = a->slopes[blockIdx.x / kSplits], ainv = a->inv_norm;
+  asm volatile("" : "+v"(aslope), "+v"(ainv));
   // fp32 granule vector (x, x1): v[c] = elements (c * 64 + lane) * 2 + {0, 1}
   auto gather_f32 = [&](size_t off, uint32_t tag, float (&v)[NP][2]) {
     uint32_t raw[NP][2];
@@ -380,20 +535,21 @@ __device__ __attribute__((noinline)) void role_gather(uint64_t ka) {
       gb[c][1] = *reinterpret_cast<const uint32_t*>(be + k);
     }
   };
-  // x (fp32, registers) -> xf; LN(x) * gamma + beta -> xa[0] (bf16)
+  // x (fp32, registers) -> xf (the block's rows); LN(x) * gamma + beta -> xa[0] (bf16)
+  const int xbase = blockIdx.x * C::RD;
   auto stage_ln = [&](float (&v)[NP][2], const uint32_t (&gb)[NP][2], float eps) {
 #pragma unroll
     for (int c = 0; c < NP; c++) {
       const int k = (c * 64 + lane) * 2;
-      *reinterpret_cast<float2*>(&sm->xf[k]) = make_float2(v[c][0], v[c][1]);
+      if ((unsigned)(k - xbase) < (unsigned)C::RD) *reinterpret_cast<float2*>(&sm->xf[k - xbase]) = make_float2(v[c][0], v[c][1]);
     }
     ln_pairs<NP>(v, eps, H);
 #pragma unroll
     for (int c = 0; c < NP; c++) {
       const int k = (c * 64 + lane) * 2;
-      const float y0 = v[c][0] * bf16_lo(gb[c][0]) + bf16_lo(gb[c][1]);
-      const float y1 = v[c][1] * bf16_hi(gb[c][0]) + bf16_hi(gb[c][1]);
-      *reinterpret_cast<uint32_t*>(&sm->xa[0][k]) = pack_bf16x2(y0, y1);
+      const f2v y = __builtin_elementwise_fma(f2v{v[c][0], v[c][1]}, f2v{bf16_lo(gb[c][0]), bf16_hi(gb[c][0])},
+                                              f2v{bf16_lo(gb[c][1]), bf16_hi(gb[c][1])});
+      *reinterpret_cast<uint32_t*>(&sm->xa[0][k]) = pack_bf16x2(y.x, y.y);
     }
   };
   for (int l = 0; l < L; l++) {
@@ -437,6 +593,10 @@ __device__ __attribute__((noinline)) void role_gather(uint64_t ka) {
       ESTAMP(l, 1);
     }
     phase_dots<H, 1>(a, sm, 0, l * C::SL + C::OQ, C::RQ, P0, sm->xa[0]);
+    // ---- B: attention part 1 (the ctx edge cannot arrive before the record edge anyway)
+    wait_ge<H>(a, sm, &sm->qkv_ready, l + 1);
+    attn_part<H>(sm, 1, ap0, anpos, ancache, aslope, ainv);
+    if (lane == 0) lds_add(&sm->att_parts, 1);
     // ---- C: ctx -> xa[1]
     gather_bf16(WO::GCTX, H, tag_of(gen, L, l, E_CTX), sm->xa[1]);
     ESTAMP(l, 2);
@@ -468,39 +628,19 @@ __device__ __attribute__((noinline)) void role_attn(uint64_t ka) {
   Smem<H>* sm = smem<H>();
   using C = Cfg<H>;
   using WO = WsOff<H>;
-  constexpr int HD = C::HD, NKV = kMaxPos * HD * 2 / 1024;  // 16-B loads per lane for a whole split of K or V
+  constexpr int HD = C::HD;
   const int lane = threadIdx.x & 63, b = blockIdx.x, head = b / kSplits, s = b % kSplits;
   const int L = a->L, mctx = a->max_ctx;
   const uint32_t gen = __builtin_amdgcn_readfirstlane(((const unsigned*)a->ws)[Ctl::GEN]);
-  const int past = a->past_dev[0];
-  const int per = (past + 1 + kSplits - 1) / kSplits;  // positions per split (<= kMaxPos)
-  const int p0 = s * per, p1 = min(p0 + per, past + 1), ncache = max(0, min(p1, past) - p0), npos = max(0, p1 - p0);
-  const int nbytes = ncache * HD * 2;
-  const float slope = a->slopes[head], inv_norm = a->inv_norm;
+  int p0, npos, ncache;
+  attn_split(a, b, p0, npos, ncache);
+  float slope = a->slopes[head], inv_norm = a->inv_norm;
+  asm volatile("" : "+v"(slope), "+v"(inv_norm));  // held in registers (else re-read from the kernarg per position)
   for (int l = 0; l < L; l++) {
     const int P0 = l * 4;
-    // the split's cached K / V rows: contiguous [ncache][HD] of this head and row (slot), requested now
-    u32x4v kr[NKV], vr[NKV];
-    {
-      const int pb = ncache > 0 ? p0 : 0;  // a split with no cached rows reads (and drops) row 0
-      const char* kl = a->kv + (size_t)l * a->kv_layer_stride + ((size_t)a->slot * kNH + head) * mctx * HD * 2 + (size_t)pb * HD * 2;
-      const char* vl = kl + a->kv_half;
-#pragma unroll
-      for (int i = 0; i < NKV; i++) {
-        const int o = min(i * 1024 + lane * 16, max(nbytes - 16, 0));
-        kr[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(kl + o));
-        vr[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(vl + o));
-      }
-    }
+    // the split's cached K / V rows arrive in sm->kv by the loader's LDS-DMA (issued before this layer's
+    // QKV slots: landed once the QKV rows below are)
     phase_dots<H, 1>(a, sm, 1, l * C::SL + C::OQ, C::RQ, P0, sm->xa[0]);
-#pragma unroll
-    for (int i = 0; i < NKV; i++) {
-      const int o = i * 1024 + lane * 16;
-      if (o < nbytes) {
-        *reinterpret_cast<u32x4v*>((char*)sm->kv[0] + o) = kr[i];
-        *reinterpret_cast<u32x4v*>((char*)sm->kv[1] + o) = vr[i];
-      }
-    }
     // the head's new q, k, v (3 HD bf16 = 3 HD / 2 granules)
     {
       constexpr int NQ = (3 * HD / 4 + 63) / 64;
@@ -514,35 +654,26 @@ __device__ __attribute__((noinline)) void role_attn(uint64_t ka) {
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) lds_put(&sm->qkv_ready, l + 1);
     ESTAMP(l, 5);
-    // scores: lane j <-> position p0 + j (ALiBi slope * position + q.k / sqrt(hd)), fp32 softmax partial
+    attn_part<H>(sm, 0, p0, npos, ncache, slope, inv_norm);
+    // the three partials -> this split's record (max, sum, acc)
+    wait_ge<H>(a, sm, &sm->att_parts, 2 * (l + 1));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     {
-      const int j = lane;
-      const bool valid = j < npos;
-      const int p = p0 + j;
-      const bf16* krow = (valid && p < past) ? sm->kv[0][j] : sm->qkv[1];
-      float d = 0.f;
+      const float m0 = sm->mg[0][0], m1 = sm->mg[1][0], m2 = sm->mg[2][0];
+      const float M = fmaxf(m0, fmaxf(m1, m2));
+      const float w0 = m0 == -INFINITY ? 0.f : __expf(m0 - M), w1 = m1 == -INFINITY ? 0.f : __expf(m1 - M),
+                  w2 = m2 == -INFINITY ? 0.f : __expf(m2 - M);
 #pragma unroll
-      for (int c = 0; c < HD / 8; c++)
-        d = dot8(*reinterpret_cast<const bf16x8*>(krow + c * 8), *reinterpret_cast<const bf16x8*>(sm->qkv[0] + c * 8), d);
-      const float sc = valid ? slope * (float)p + inv_norm * d : -INFINITY;
-      const float mx = wave_max(sc);
-      const float e = valid ? __expf(sc - mx) : 0.f;
-      const float lsum = wave_sum(e);
-      sm->pr[j] = e;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      // acc[d] = sum_j pr[j] v_j[d]: lane t takes dims t and t + 64
-      float acc0 = 0.f, acc1 = 0.f;
-      const int d0 = lane, d1 = lane + 64;
-      for (int jj = 0; jj < npos; jj++) {
-        const float pj = sm->pr[jj];
-        const bf16* vrow = (p0 + jj < past) ? sm->kv[1][jj] : sm->qkv[2];
-        if (d0 < HD) acc0 += pj * (float)vrow[d0];
-        if (d1 < HD) acc1 += pj * (float)vrow[d1];
+      for (int h2 = 0; h2 < 2; h2++) {
+        const int d = lane + 64 * h2;
+        if (d < HD) sm->rec[2 + d] = w0 * sm->mg[0][2 + d] + w1 * sm->mg[1][2 + d] + w2 * sm->mg[2][2 + d];
       }
-      if (d0 < HD) sm->rec[2 + d0] = acc0;
-      if (d1 < HD) sm->rec[2 + d1] = acc1;
-      if (lane == 0) { sm->rec[0] = npos > 0 ? mx : -INFINITY; sm->rec[1] = lsum; }
+      if (lane == 0) {
+        sm->rec[0] = npos > 0 ? M : -INFINITY;
+        sm->rec[1] = w0 * sm->mg[0][1] + w1 * sm->mg[1][1] + w2 * sm->mg[2][1];
+      }
       if (lane == 0) lds_put(&sm->att_ready, l + 1);
       ESTAMP(l, 6);
     }
@@ -601,6 +732,10 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
   const size_t ls = a->layer_stride;
   const uint32_t gen = __builtin_amdgcn_readfirstlane(((const unsigned*)a->ws)[Ctl::GEN]);
   char* ws = a->ws;
+  int ap0, anpos, ancache;
+  attn_split(a, b, ap0, anpos, ancache);
+  float aslope = a->slopes[head], ainv = a->inv_norm;
+  asm volatile("" : "+v"(aslope), "+v"(ainv));
   // this lane's rows of each epilogue (lanes past a phase's rows compute row 0 and never store)
   const int jq = 2 * min(lane, C::RQ / 2 - 1), jd = min(lane, C::RD - 1), j1 = 2 * min(lane, C::R1 / 2 - 1),
             j2 = min(lane, C::R2 - 1);
@@ -618,7 +753,6 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
     phase_dots<H, 1>(a, sm, 2, g0 + C::OQ, C::RQ, P0, sm->xa[0]);
     wait_ge<H>(a, sm, &sm->dots_done, 3 * (P0 + 1));
     ESTAMP(l, 8);
-    lds_put(&sm->freed, g0 + C::OD);
     if (lane < C::RQ / 2) {
       const float v0 = sm->res[jq] + bf16_lo(bq), v1 = sm->res[jq + 1] + bf16_hi(bq);
       const uint32_t pk = pack_bf16x2(v0, v1);
@@ -629,7 +763,10 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
       put_granule(ws + WO::GQKV + (size_t)(nq / 2) * 8, tag_of(gen, L, l, E_QKV), pk);
     }
     ESTAMP(l, 9);
-    // ---- B: this split's record; the head's context (split 0)
+    // ---- B: attention part 2; this split's record; the head's context (split 0)
+    wait_ge<H>(a, sm, &sm->qkv_ready, l + 1);
+    attn_part<H>(sm, 2, ap0, anpos, ancache, aslope, ainv);
+    if (lane == 0) lds_add(&sm->att_parts, 1);
     wait_ge<H>(a, sm, &sm->att_ready, l + 1);
     {
       const uint32_t tp = tag_of(gen, L, l, E_PART);
@@ -651,15 +788,13 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
     // ---- C: dense -> x1 = x + dense(ctx) + bias
     phase_dots<H, 1>(a, sm, 2, g0 + C::OD, C::RD, P0 + 1, sm->xa[1]);
     wait_ge<H>(a, sm, &sm->dots_done, 3 * (P0 + 2));
-    lds_put(&sm->freed, g0 + C::O1);
     if (lane < C::RD)
       put_granule(ws + WO::GX1 + (size_t)nd * 8, tag_of(gen, L, l, E_X1),
-                  __float_as_uint((sm->res[jd] + bf16_lo(bd)) + sm->xf[nd]));
+                  __float_as_uint((sm->res[jd] + bf16_lo(bd)) + sm->xf[jd]));
     ESTAMP(l, 12);
     // ---- D: fc1 + bias, GELU -> g
     phase_dots<H, 1>(a, sm, 2, g0 + C::O1, C::R1, P0 + 2, sm->xa[0]);
     wait_ge<H>(a, sm, &sm->dots_done, 3 * (P0 + 3));
-    lds_put(&sm->freed, g0 + C::O2);
     if (lane < C::R1 / 2)
       put_granule(ws + WO::GG + (size_t)(n1 / 2) * 8, tag_of(gen, L, l, E_G),
                   pack_bf16x2(gelu_bloom(sm->res[j1] + bf16_lo(b1)), gelu_bloom(sm->res[j1 + 1] + bf16_hi(b1))));
@@ -667,9 +802,8 @@ __device__ __attribute__((noinline)) void role_publish(uint64_t ka) {
     // ---- E: fc2 -> x = x1 + fc2(g) + bias (the last layer writes the stage output)
     phase_dots<H, 4>(a, sm, 2, g0 + C::O2, C::R2, P0 + 3, sm->xg);
     wait_ge<H>(a, sm, &sm->dots_done, 3 * (P0 + 4));
-    lds_put(&sm->freed, g0 + C::SL);
     if (lane < C::R2) {
-      const float y = (sm->res[j2] + bf16_lo(b2)) + sm->xf[n2];
+      const float y = (sm->res[j2] + bf16_lo(b2)) + sm->xf[j2];
       if (l + 1 == L) a->x_out[n2] = y;
       else put_granule(ws + WO::GX + (size_t)n2 * 8, tag_of(gen, L, l, E_X), __float_as_uint(y));
     }
@@ -693,8 +827,8 @@ template <int H>
 __global__ __launch_bounds__(kThreads) void decode_engine_kernel(EngineArgs a) {
   Smem<H>* sm = smem<H>();
   if (threadIdx.x == 0) {
-    sm->landed = 0; sm->freed = 0; sm->dots_done = 0; sm->in_ready = 0; sm->att_ready = 0; sm->merge_ready = 0;
-    sm->dead = 0; sm->gathering = 0;
+    sm->landed = 0; sm->need[0] = 0; sm->need[1] = 0; sm->need[2] = 0; sm->dots_done = 0; sm->in_ready = 0; sm->att_ready = 0; sm->merge_ready = 0;
+    sm->dead = 0; sm->gathering = 0; sm->qkv_ready = 0; sm->att_parts = 0;
   }
   __syncthreads();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

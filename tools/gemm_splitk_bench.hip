@@ -1,5 +1,5 @@
-// tools/gemm_splitk_bench.hip — prefill GEMM variants on the BLOOM prefill shapes (M tokens x N x K), HIP events,
-// median of 20 launches each: the library's dispatch (launch_linear), the round-2 tiles (64x64 / 64x32, 4-deep
+// tools/gemm_splitk_bench.hip — prefill GEMM variants on the BLOOM prefill shapes (M tokens x N x K), HIP events
+// around 20 back-to-back launches (median of 7): the library's dispatch (launch_linear), the round-2 tiles (64x64 / 64x32, 4-deep
 // ring) and 128x128 tiles with split-K KS = 1, 2, 3, 4, 6.  Every split-K output is checked against KS = 1 (the
 // same products summed in another order: max relative difference printed); gemm_mfma3 (128x128 tiles on
 // v_mfma_f32_32x32x16_bf16, stream-K) at grids of 128..512 blocks.
@@ -38,12 +38,17 @@ int main() {
     Epi ep{};
     ep.kind = EPI_RESID; ep.bias = bias; ep.out_f32 = out; ep.resid = resid; ep.ldo = N;
     ep.sk_ws = ws; ep.sk_tickets = tick; ep.sk_cap = cap; ep.sk_ntickets = 4096;
+    // per launch: 20 launches back to back between two events (as tools/gemm_shapes_torch.py times hipBLASLt:
+    // a lone launch between events also counts the ~5 us the events add), median of 7 such runs
     auto timeit = [&](auto&& fn) {
       std::vector<float> t;
-      for (int it = 0; it < 25; it++) {
-        CK(hipEventRecord(e0)); fn(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      for (int i = 0; i < 5; i++) fn();
+      for (int it = 0; it < 7; it++) {
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < 20; i++) fn();
+        CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-        if (it >= 5) t.push_back(ms * 1e3f);
+        t.push_back(ms * 1e3f / 20);
       }
       std::sort(t.begin(), t.end());
       return t[t.size() / 2];

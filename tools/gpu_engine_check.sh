@@ -7,7 +7,7 @@ rm -f $BS_PARITY_LOG
 timeout -k 10 400 python -u -m pytest tests/test_gpu_engine.py -v -x --timeout 120 --timeout-method thread > gpurun_out/r4e_pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/r4e_pytest.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-for V in d8 d4 d16 thin; do
+for V in d8 d12 d4 thin2; do
   echo "== $V" >> gpurun_out/r4e_timeline.txt
   timeout -k 10 60 ./tools/engine_timeline_$V 580 >> gpurun_out/r4e_timeline.txt 2>&1 || exit 1
 done
