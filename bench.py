@@ -38,8 +38,6 @@ def parse(argv=None):
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU checker on a bounded sample")
     p.add_argument("--cpu-steps", type=int, default=24)
     p.add_argument("--no-profile", action="store_true")
-    p.add_argument("--engine", type=int, default=None,
-                   help="decode engine (bs_set_decode_engine): 1 on, 0 per-block launches; default: the library's")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     p.add_argument("--no-head-split", action="store_true", help="pipeline: keep the whole lm_head on the last stage")
     p.add_argument("--pipeline", action="store_true",
@@ -258,8 +256,6 @@ def bench_single(args):
     st = Stage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, m.n_layer, dtype=args.dtype, device=0, max_batch=B,
                max_ctx=max_ctx, max_tokens=max(B * P, B), seed=args.seed,
                int8_weights=args.weights == "int8" or m.int8_weights)
-    if args.engine is not None:
-        st.set_decode_engine(bool(args.engine))
     wbytes = st.info()["weight_bytes"]
     cs = torch.cuda.Stream()  # a real stream (the legacy default stream cannot be graph-captured)
     with torch.cuda.stream(cs):

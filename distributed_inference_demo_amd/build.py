@@ -17,7 +17,7 @@ LIB = os.path.join(PKG, "lib", "libbloomstage.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "engine.hip", "stage.hip", "codec.cpp", "safetensors.cpp"]
+SOURCES = ["kernels.hip", "stage.hip", "codec.cpp", "safetensors.cpp"]
 HEADERS = ["common.h", "kernels.h", "attn_merge.h", "safetensors.h"]
 STAMP = os.path.join(OBJ, "build_id")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",

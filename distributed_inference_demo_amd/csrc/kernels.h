@@ -154,29 +154,3 @@ void launch_linear_q8_ln(const float* x, int row_stride, int row_offset, const v
 // LayerNorm of M fp32 rows -> bf16 (register-resident one-block-per-row kernel when K <= 4096).
 void launch_ln_rows(const float* x, int row_stride, int row_offset, const void* gamma, const void* beta, float eps,
                     void* out_bf16, int M, int K, hipStream_t s);
-
-// ---- Persistent decode engine (engine.hip): every decoder block of a bf16 stage for one decode step
-// (S = 1, one row, hidden 1024 / 1536, 16 heads, contexts <= 1024) in one launch of one workgroup per CU; an
-// LDS-DMA loader wave streams the block's weights ahead of the dependency edges.  Layer l's tensor t is at
-// (layer-0 pointer) + l * layer_stride bytes.
-struct EngineArgs {
-  const char* wl;          // layer 0's tensors (arena order, engine.hip LayerOff); layer l at + l * layer_stride
-  size_t layer_stride;
-  const char* kv;          // KV cache of layer 0: K at kv, V at kv + kv_half; layer l at + l * kv_layer_stride
-  size_t kv_layer_stride, kv_half;
-  int L, M, h, n_head, hd, max_ctx, slot;
-  float eps, inv_norm;
-  const float* slopes;     // [n_head]
-  const int* past_dev;     // [M] cached length of each row
-  const float* x_in;       // [M][h] fp32 stage input, or null on the first stage:
-  const int* ids;          //   token ids [M] -> word_embeddings + word_embeddings_layernorm
-  const void *wemb, *emb_g, *emb_b;
-  float* x_out;            // [M][h] fp32 stage output (residual stream after the last block)
-  char* ws;                // engine_ws_bytes(h, n_head), zeroed once at init: control words + granule buffers
-  unsigned* sticky_host;   // host-mapped error word: 1 once any in-kernel wait expired (never reset)
-};
-size_t engine_status_offset();  // byte offset in EngineArgs::ws of the sticky timeout word
-size_t engine_ws_bytes(int h, int n_head);
-size_t engine_layer_bytes(int h);  // bytes of one layer's tensors in the arena (the offsets the kernel assumes)
-bool engine_supported(int device, int M, int h, int n_head, int max_ctx);
-void launch_decode_engine(const EngineArgs& a, hipStream_t s);

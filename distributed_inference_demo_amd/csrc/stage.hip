@@ -134,14 +134,7 @@ struct bs_stage {
   float temperature = 1.f;
   uint64_t sample_seed = 0;
   float* sample_logits = nullptr;   // [max_batch][V] logits the sampler reads (device I/O without logits)
-  // decode engine (engine.hip): workspace when the stage's shape allows it; on/off (bs_set_decode_engine)
-  char* eng_ws = nullptr;
-  unsigned* eng_sticky = nullptr;   // host-mapped: 1 once an in-kernel wait of the engine expired (never reset)
-  unsigned* eng_sticky_dev = nullptr;
-  size_t eng_layer_bytes = 0;
-  int eng_on = 0;                   // bs_set_decode_engine (off until it beats the launches)
   int graphs_on = 1;                // bs_set_graphs: decode steps on device buffers replay captured graphs
-  int eng_used = 0;                 // the last enqueued forward took the engine
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -252,8 +245,6 @@ static void free_stage(bs_stage* s) {
   if (s->logit_buf) hipFree(s->logit_buf);
   if (s->sample_logits) hipFree(s->sample_logits);
   if (s->wtmp) hipFree(s->wtmp);
-  if (s->eng_ws) hipFree(s->eng_ws);
-  if (s->eng_sticky) hipHostFree(s->eng_sticky);
   if (s->own) hipStreamDestroy(s->own);
   delete s;
 }
@@ -614,21 +605,6 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   s->sk_ws = (float*)(s->ws + wo[wi++]);
   s->sk_tickets = (unsigned*)(s->ws + wo[wi++]);
   HIP_TRY(hipMemsetAsync(s->ws, 0, s->wsbytes, s->own));
-  // decode engine: bf16 block weights at the arena offsets engine.hip assumes (checked, not trusted)
-  if (s->bf16 && !s->q8 && s->L > 0 && (h == 1024 || h == 1536)) {
-    const size_t lb = engine_layer_bytes((int)h);
-    bool ok = (char*)s->layers[0].t[T_FC2_B] + h * 2 - (char*)s->layers[0].t[T_LN1_G] == (ptrdiff_t)lb;
-    for (int l = 1; l < s->L && ok; l++) ok = (char*)s->layers[l].t[T_LN1_G] - (char*)s->layers[0].t[T_LN1_G] == (ptrdiff_t)(l * lb);
-    const size_t eb = engine_ws_bytes((int)h, desc->n_head);
-    if (ok && hipMalloc((void**)&s->eng_ws, eb) == hipSuccess) {
-      s->eng_layer_bytes = lb;
-      HIP_TRY(hipMemsetAsync(s->eng_ws, 0, eb, s->own));
-      if (hipHostMalloc((void**)&s->eng_sticky, 4, hipHostMallocMapped) == hipSuccess) {
-        *s->eng_sticky = 0;
-        if (hipHostGetDevicePointer((void**)&s->eng_sticky_dev, s->eng_sticky, 0) != hipSuccess) s->eng_sticky_dev = nullptr;
-      }
-    }
-  }
   std::vector<float> sl(desc->n_head);
   alibi_slopes(desc->n_head, sl.data());
   HIP_TRY(hipMemcpyAsync(s->slopes, sl.data(), sl.size() * 4, hipMemcpyHostToDevice, s->own));
@@ -1069,8 +1045,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
       HIP_TRY(hipMemcpyAsync(s->ids, ids, (size_t)M * 4, hipMemcpyHostToDevice, st));
       ids = s->ids;
     }
-    const bool eng = S == 1 && s->eng_ws && s->eng_on && engine_supported(d.device, M, h, d.n_head, d.max_ctx);
-    if (!emb_fused && !eng) launch_layernorm(s->bf16, s->wemb, ids, 0, 0, s->emb_g, s->emb_b, s->xa, 1, M, h, d.ln_eps, st);
+    if (!emb_fused) launch_layernorm(s->bf16, s->wemb, ids, 0, 0, s->emb_g, s->emb_b, s->xa, 1, M, h, d.ln_eps, st);
     cur = s->xa;
   } else if (host_io) {
     HIP_TRY(hipMemcpyAsync(s->xa, in, (size_t)M * h * 4, hipMemcpyHostToDevice, st));
@@ -1081,29 +1056,7 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
 
   // ---- decoder blocks
   const float inv_norm = 1.0f / std::sqrt((float)hd);
-  s->eng_used = 0;
-  if (S == 1 && s->eng_ws && s->eng_on && engine_supported(d.device, M, h, nh, d.max_ctx)) {
-    // every block in one persistent launch (engine.hip); the first stage gathers its embeddings there
-    EngineArgs ea{};
-    ea.wl = (const char*)s->layers[0].t[T_LN1_G];
-    ea.layer_stride = s->eng_layer_bytes;
-    ea.kv = s->kv; ea.kv_layer_stride = s->kv_layer_stride; ea.kv_half = s->kv_half;
-    ea.L = s->L; ea.M = M; ea.h = h; ea.n_head = nh; ea.hd = hd; ea.max_ctx = d.max_ctx; ea.slot = slot;
-    ea.eps = d.ln_eps; ea.inv_norm = inv_norm; ea.slopes = s->slopes; ea.past_dev = past_dev;
-    ea.x_in = d.is_first ? nullptr : cur;
-    ea.ids = ids; ea.wemb = s->wemb; ea.emb_g = s->emb_g; ea.emb_b = s->emb_b;
-    ea.x_out = (!d.is_last && !host_io) ? (float*)out : (cur == s->xb ? s->xa : s->xb);
-    ea.ws = s->eng_ws;
-    ea.sticky_host = s->eng_sticky_dev;
-    double wbytes = (double)s->L * (12.0 * h * h + 13.0 * h) * 2.0;
-    {
-      ProfScope p(s, st, 1, wbytes + ctx_sum * nh * hd * 2 * s->esz + (double)M * h * 4 * 2);
-      launch_decode_engine(ea, st);
-    }
-    cur = ea.x_out;
-    s->eng_used = 1;
-  }
-  for (int l = 0; l < s->L && !s->eng_used; l++) {
+  for (int l = 0; l < s->L; l++) {
     const Layer& w = s->layers[l];
     char* kbase = s->kv + l * s->kv_layer_stride;
     // x1 = LN_in(x); fused QKV (+bias) -> q, K/V cache
@@ -1246,43 +1199,6 @@ extern "C" int bs_set_sampling(bs_stage* s, int32_t top_k, float temperature, ui
   return BS_OK;
 }
 
-extern "C" int bs_set_decode_engine(bs_stage* s, int32_t on) {
-  if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
-  HIP_TRY(hipSetDevice(s->d.device));
-  HIP_TRY(hipDeviceSynchronize());
-  for (auto& g : s->graphs) hipGraphExecDestroy(g.second);
-  s->graphs.clear();
-  s->eng_on = on ? 1 : 0;
-  return BS_OK;
-}
-
-extern "C" int bs_engine_status(bs_stage* s, int32_t* used, int32_t* status) {
-  if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
-  HIP_TRY(hipSetDevice(s->d.device));
-  HIP_TRY(hipStreamSynchronize(s->own));
-  HIP_TRY(hipDeviceSynchronize());
-  if (used) *used = s->eng_used;
-  if (status) {
-    *status = 0;
-    if (s->eng_ws) {
-      // the sticky timeout word: set by any launch whose in-kernel wait expired, never reset
-      uint32_t w = 0;
-      HIP_TRY(hipMemcpy(&w, s->eng_ws + engine_status_offset(), 4, hipMemcpyDeviceToHost));
-      *status = (int32_t)(w | (s->eng_sticky ? *(volatile unsigned*)s->eng_sticky : 0u));
-    }
-  }
-  return BS_OK;
-}
-
-// diagnostics (tools/diag_engine.py only; not part of the ABI): the engine's raw sync words
-extern "C" int bs_debug_engine_sync(bs_stage* s, uint32_t* out, int32_t n) {
-  if (!s || !s->eng_ws) return fail(BS_ERR_STATE, "no engine workspace");
-  HIP_TRY(hipDeviceSynchronize());
-  const size_t nb = std::min((size_t)n * 4, (size_t)256);  // the control words
-  HIP_TRY(hipMemcpy(out, s->eng_ws, nb, hipMemcpyDeviceToHost));
-  return (int)(nb / 4);
-}
-
 extern "C" int bs_set_graphs(bs_stage* s, int32_t on) {
   if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
   HIP_TRY(hipSetDevice(s->d.device));
@@ -1307,8 +1223,6 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
   }
   if (M > d.max_tokens) return fail(BS_ERR_INVALID, "batch*seq exceeds max_tokens");
   if (!in || !out) return fail(BS_ERR_INVALID, "in/out is NULL");
-  if (s->eng_sticky && *(volatile unsigned*)s->eng_sticky)
-    return fail(BS_ERR_DEVICE, "decode engine: an in-kernel wait expired in an earlier step (its outputs were garbage)");
   const bool want_logits = (step->flags & BS_STEP_LOGITS) != 0;
   if (want_logits && (!d.is_last || !logits)) return fail(BS_ERR_INVALID, "logits requested on a non-last stage or NULL");
   const bool host_io = (step->flags & BS_STEP_HOST_IO) != 0;

@@ -383,8 +383,6 @@ def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb
                    device=device.index if device.type == "cuda" else 0, max_batch=mb_rows * n_mb,
                    max_ctx=max_ctx, max_tokens=mb_rows * max_seq, seed=seed, is_first=is_first,
                    is_last=is_last and not head_split, head_slice=hslice, int8_weights=model.int8_weights)
-        if world > 1:  # the persistent decode engine needs every CU; RCCL kernels on other streams hold some
-            st.set_decode_engine(False)
         ex = StageExecutor(st)
     else:
         ex = executor_factory(lb, le, is_first, is_last and not head_split, mb_rows * n_mb, max_ctx, hslice)

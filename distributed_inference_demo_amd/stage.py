@@ -82,7 +82,7 @@ EXPORTS = [
     "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
     "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice", "bs_stream_delay", "bs_set_sampling",
     "bs_build_id", "bs_hbm_probe", "bs_mfma_probe", "bs_init_stage_file", "bs_weights_file_probe",
-    "bs_set_decode_engine", "bs_engine_status", "bs_set_graphs",
+    "bs_set_graphs",
 ]
 
 _LIB = None
@@ -134,9 +134,7 @@ def lib():
         L.bs_head_norm.argtypes = [vp, vp, i32, i32, vp, vp]
         L.bs_head_slice.argtypes = [vp, vp, i32, vp, vp, vp, vp]
         L.bs_set_sampling.argtypes = [vp, i32, ctypes.c_float, ctypes.c_uint64]
-        L.bs_set_decode_engine.argtypes = [vp, i32]
         L.bs_set_graphs.argtypes = [vp, i32]
-        L.bs_engine_status.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.bs_hbm_probe.argtypes = [i32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.bs_mfma_probe.argtypes = [i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         _LIB = L
@@ -248,16 +246,6 @@ class Stage:
     def set_graphs(self, on=True):
         """bs_set_graphs: replay captured decode graphs (default) or launch every step eagerly."""
         _check(lib().bs_set_graphs(self._h, 1 if on else 0))
-
-    def set_decode_engine(self, on=True):
-        """bs_set_decode_engine: the persistent decode engine (default off) or the per-block launches."""
-        _check(lib().bs_set_decode_engine(self._h, 1 if on else 0))
-
-    def engine_status(self):
-        """(used, status) of the last forward: whether it ran the decode engine, and its timeout word."""
-        used, status = ctypes.c_int32(0), ctypes.c_int32(0)
-        _check(lib().bs_engine_status(self._h, ctypes.byref(used), ctypes.byref(status)))
-        return used.value, status.value
 
     # ---- vocabulary-parallel head (device pointers, stream ordered)
     def head_norm(self, hidden, batch, seq, xn, stream=None):

@@ -175,21 +175,6 @@ int bs_set_sampling(bs_stage *stage, int32_t top_k, float temperature, uint64_t 
  * debugging and A/B timing).  Drops captured graphs.  Returns BS_OK. */
 int bs_set_graphs(bs_stage *stage, int32_t on);
 
-/* ---- Decode engine ----
- * bf16 stages of hidden 1024 or 1536 (bloom-560m / bloom-1b1 widths), 16 heads, max_ctx <= 1024, run a
- * decode step of ONE row (S = 1) as one persistent launch of every decoder block (one workgroup per CU, an
- * LDS-DMA loader wave streaming the weights ahead of the dependency edges) instead of five launches per
- * block.  The launch needs all 256 workgroups resident at once: do not enable it on a stage whose GPU
- * runs other kernels concurrently (the multi-rank pipeline, whose RCCL kernels hold CUs, keeps it off).
- * on = 1 uses it where it applies, 0 always takes the per-block launches.  Captured decode graphs are
- * dropped.  Returns BS_OK. */
-int bs_set_decode_engine(bs_stage *stage, int32_t on);
-/* *used = 1 if the last forward took the engine; *status = the stage's sticky timeout word (0 = every
- * in-kernel hand-off of every engine launch completed; nonzero = a wait expired after 200 ms in some
- * launch and that step's results were invalid).  The word is never reset: once set, bs_forward refuses
- * the stage (BS_ERR_DEVICE).  Synchronizes the stage's stream.  For tests and diagnostics. */
-int bs_engine_status(bs_stage *stage, int32_t *used, int32_t *status);
-
 /* Forget the cached positions of one KV row (slot), or of all rows when slot < 0. */
 int bs_reset_kv(bs_stage *stage, int32_t slot);
 /* Read back KV row `slot` of the stage's local layer `layer`, positions [pos0, pos0 + npos), as fp32

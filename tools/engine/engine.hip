@@ -1,5 +1,9 @@
-// engine.hip — the persistent decode engine: every decoder block of a stage for one decode step of ONE row
-// (S = 1, M = 1, bf16, hidden 1024 / 1536, 16 heads) in one launch on gfx950.
+// tools/engine/engine.hip — the persistent decode engine: every decoder block of a stage for one decode step of
+// ONE row (S = 1, M = 1, bf16, hidden 1024 / 1536, 16 heads) in one launch on gfx950.
+// NOT part of the library: measured at parity with the five-launch decode path at best
+// (profiles/r04_engine_timeline_ab.txt), it was moved out in round 4 and is kept as the A/B experiment that
+// tools/engine_timeline.hip builds (the stage's host integration and parity tests were removed with it; the
+// last library version with them is in git history).
 //
 // Why: at batch 1 a bloom-1b1 layer is five dependent weight-streaming launches (LN+QKV 5.4, attention 4.8,
 // dense 4.8, LN+fc1 5.4, fc2 5.1 us) moving 56.6 MB -- 8.7 us of HBM streaming at 6.5 TB/s; the rest is kernel
@@ -40,8 +44,34 @@
 // later wait falls through, the grid drains), ORs 1 into the stage's sticky error word (host-mapped, never
 // reset: bs_forward refuses to run once it is set) and the step's outputs are garbage.  The grid assumes all
 // 256 workgroups resident: the stage refuses the engine inside a multi-rank pipeline (RCCL kernels hold CUs).
-#include "common.h"
-#include "kernels.h"
+#include "../../distributed_inference_demo_amd/csrc/common.h"
+#include "../../distributed_inference_demo_amd/csrc/kernels.h"
+
+// ---- Persistent decode engine: every decoder block of a bf16 stage for one decode step
+// (S = 1, one row, hidden 1024 / 1536, 16 heads, contexts <= 1024) in one launch of one workgroup per CU; an
+// LDS-DMA loader wave streams the block's weights ahead of the dependency edges.  Layer l's tensor t is at
+// (layer-0 pointer) + l * layer_stride bytes.
+struct EngineArgs {
+  const char* wl;          // layer 0's tensors (arena order, engine.hip LayerOff); layer l at + l * layer_stride
+  size_t layer_stride;
+  const char* kv;          // KV cache of layer 0: K at kv, V at kv + kv_half; layer l at + l * kv_layer_stride
+  size_t kv_layer_stride, kv_half;
+  int L, M, h, n_head, hd, max_ctx, slot;
+  float eps, inv_norm;
+  const float* slopes;     // [n_head]
+  const int* past_dev;     // [M] cached length of each row
+  const float* x_in;       // [M][h] fp32 stage input, or null on the first stage:
+  const int* ids;          //   token ids [M] -> word_embeddings + word_embeddings_layernorm
+  const void *wemb, *emb_g, *emb_b;
+  float* x_out;            // [M][h] fp32 stage output (residual stream after the last block)
+  char* ws;                // engine_ws_bytes(h, n_head), zeroed once at init: control words + granule buffers
+  unsigned* sticky_host;   // host-mapped error word: 1 once any in-kernel wait expired (never reset)
+};
+size_t engine_status_offset();  // byte offset in EngineArgs::ws of the sticky timeout word
+size_t engine_ws_bytes(int h, int n_head);
+size_t engine_layer_bytes(int h);  // bytes of one layer's tensors in the arena (the offsets the kernel assumes)
+bool engine_supported(int device, int M, int h, int n_head, int max_ctx);
+void launch_decode_engine(const EngineArgs& a, hipStream_t s);
 
 namespace {
 

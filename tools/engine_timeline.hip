@@ -6,7 +6,7 @@
 // "seen" stamp.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -DBS_ENGINE_STAMPS tools/engine_timeline.hip -o tools/engine_timeline
 #define BS_ENGINE_STAMPS 1
-#include "../distributed_inference_demo_amd/csrc/engine.hip"
+#include "engine/engine.hip"
 #include <algorithm>
 #include <cstdio>
 #include <vector>
