@@ -1616,7 +1616,13 @@ __device__ unsigned long long g_gemm3_stamps[4096 * 4];
 __host__ __device__ __forceinline__ long gemm3_first(int bb, long T, int G) { return (long)bb * T / G; }
 __host__ __device__ __forceinline__ int gemm3_owner(long x, long T, int G) { return (int)(((x + 1) * G + T - 1) / T - 1); }
 
-template <int EK, int NSTG = 3>  // NSTG LDS stages: 3 (96 KB, one block per CU) or 2 (64 KB, two per CU)
+// XCD-aware placement (XM): workgroups are dispatched round-robin over the 8 XCDs (block i on XCD i % 8), each
+// XCD with its own 4 MB L2.  Virtual block v = (i % 8) * (G / 8) + i / 8 gives every XCD one contiguous eighth
+// of the iteration space, and tiles are numbered column-major (all M tiles of a W column tile in a row), so an
+// XCD streams ~1/8 of W (+ all of X) instead of every XCD streaming all of W from the Infinity Cache.
+__host__ __device__ __forceinline__ int gemm3_vblock(int i, int G) { return G % 8 ? i : (i % 8) * (G / 8) + i / 8; }
+
+template <int EK, int NSTG = 3, bool XM = true>  // NSTG LDS stages: 3 (96 KB, one block per CU) or 2 (64 KB, two per CU)
 __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                                          int M, int N, int K, Epi ep) {
   constexpr int BM = 128, BN = 128, BK = 64;
@@ -1625,9 +1631,9 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
   __shared__ __attribute__((aligned(16))) bf16 smem[NSTG * (BM + BN) * BK];  // 96 KB, the only LDS object
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3, r = lane & 31, h = lane >> 5;  // wave tile 64 x 32 at (64 wm, 32 wn)
-  const int tiles_n = (N + BN - 1) / BN, nk = K / BK;
-  const long T = (long)tiles_n * ((M + BM - 1) / BM) * nk;
-  const int G = gridDim.x, b = blockIdx.x;
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM, nk = K / BK;
+  const long T = (long)tiles_n * tiles_m * nk;
+  const int G = gridDim.x, b = XM ? gemm3_vblock(blockIdx.x, G) : blockIdx.x;
   const long it_begin = gemm3_first(b, T, G), it_end = gemm3_first(b + 1, T, G);
 #ifdef GEMM3_STAMPS
   const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
@@ -1651,7 +1657,8 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
   for (long it = it_begin; it < it_end;) {
     const int t = (int)(it / nk), k0 = (int)(it - (long)t * nk);
     const int kn = (int)min((long)(nk - k0), it_end - it);  // K-steps of this segment
-    const int tm = t / tiles_n, m0 = tm * BM, n0 = (t - tm * tiles_n) * BN;
+    const int tn = XM ? t / tiles_m : t - (t / tiles_n) * tiles_n, tm = XM ? t - tn * tiles_m : t / tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
     const bool first_seg = it == it_begin;
     it += kn;
     uint32_t oa[CA], ob[CB];
@@ -1870,12 +1877,12 @@ static int gemm3_grid(int M, int N, int K, const Epi& ep) {
   return (int)G;
 }
 
-template <int NSTG = 3>
+template <int NSTG = 3, bool XM = true>
 static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int G) {
   switch (ep.kind) {
-    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, NSTG><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
-    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, NSTG><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
-    default: gemm_mfma3_kernel<EPI_GELU, NSTG><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, NSTG, XM><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, NSTG, XM><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    default: gemm_mfma3_kernel<EPI_GELU, NSTG, XM><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
   }
 }
 

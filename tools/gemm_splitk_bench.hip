@@ -2,7 +2,8 @@
 // around 20 back-to-back launches (median of 7): the library's dispatch (launch_linear), the round-2 tiles (64x64 / 64x32, 4-deep
 // ring) and 128x128 tiles with split-K KS = 1, 2, 3, 4, 6.  Every split-K output is checked against KS = 1 (the
 // same products summed in another order: max relative difference printed); gemm_mfma3 (128x128 tiles on
-// v_mfma_f32_32x32x16_bf16, stream-K) at grids of 128..512 blocks.
+// v_mfma_f32_32x32x16_bf16, stream-K) at the dispatch's grid with and without the XCD-aware placement (XM), and at
+// grids of 192..512 blocks.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/gemm_splitk_bench.hip -o tools/gemm_splitk_bench
 #include "../distributed_inference_demo_amd/csrc/kernels.hip"
 #include <algorithm>
@@ -78,6 +79,21 @@ int main() {
     };
     for (int ks : {1, 4})
       variant("64x64 r4", 64, 64, ks, [&] { gemm2_launch<64, 64, 4>(X, W, M, N, K, ep, 0, ks); });
+    if (const int G = gemm3_grid(M, N, K, ep)) {
+      for (int xm = 0; xm < 2; xm++) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "m32 dispatch G=%d XM=%d", G, xm);
+        const float us = timeit([&] {
+          if (xm) gemm3_launch<3, true>(X, W, M, N, K, ep, 0, G);
+          else gemm3_launch<3, false>(X, W, M, N, K, ep, 0, G);
+        });
+        CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
+        double md = 0;
+        for (size_t i = 0; i < ho.size(); i++) md = std::max(md, (double)fabsf(ho[i] - hr[i]));
+        line(nm, us);
+        if (md > 1e-3) printf("           MISMATCH max |diff| %.3g\n", md);
+      }
+    }
     for (int v = 0; v < 6; v++) {
       const int G = v < 3 ? (int[]){192, 256, 384}[v] : (int[]){256, 384, 512}[v - 3];
       const int nst = v < 3 ? 3 : 2;
