@@ -72,7 +72,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
             if err and verbose:
                 print(err)
     if jobs or not os.path.exists(LIB) or any(_mtime(o) > _mtime(LIB) for o in objs):
-        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs)
+        # -z defs: an unresolved symbol (e.g. a kernel launch stub the host pass dropped) fails the link
+        # instead of shipping a library that fails at load time
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-z,defs", "-o", LIB] + objs)
     with open(STAMP, "w") as f:
         f.write(bid)
     return LIB

@@ -1622,15 +1622,22 @@ __host__ __device__ __forceinline__ int gemm3_owner(long x, long T, int G) { ret
 // XCD streams ~1/8 of W (+ all of X) instead of every XCD streaming all of W from the Infinity Cache.
 __host__ __device__ __forceinline__ int gemm3_vblock(int i, int G) { return G % 8 ? i : (i % 8) * (G / 8) + i / 8; }
 
-template <int EK, int NSTG = 3, bool XM = true>  // NSTG LDS stages: 3 (96 KB, one block per CU) or 2 (64 KB, two per CU)
+// NSTG LDS stages: 3 (one block per CU) or 2 (two per CU at BN = 128).  BN_ = 128: 8 waves of 64 x 32; BN_ = 256
+// (wide tiles for wide N: bloom-7b1's QKV / fc1 at 512 tokens are 192 / 256 whole 128 x 256 tiles, one per CU, no
+// partial tiles, a third less staging per MFMA): 8 waves of 64 x 64, 144 KB of LDS.
+template <int EK, int NSTG = 3, bool XM = true, int BN_ = 128>
 __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                                          int M, int N, int K, Epi ep) {
-  constexpr int BM = 128, BN = 128, BK = 64;
+#if defined(__HIP_DEVICE_COMPILE__)  // the host pass dropped this template's launch stubs (no diagnostic) without it
+  constexpr int BM = 128, BN = BN_, BK = 64;
+  constexpr int FJ = BN / 128, WNC = BN / 4;     // 32-column fragments per wave, columns per wave
   constexpr int NTH = 512;                       // 8 waves: 2 per SIMD, one's MFMAs cover the other's LDS waits
-  constexpr int CA = BM * BK / 8 / NTH, CB = BN * BK / 8 / NTH;  // 16-B chunks per thread per stage: 2, 2
-  __shared__ __attribute__((aligned(16))) bf16 smem[NSTG * (BM + BN) * BK];  // 96 KB, the only LDS object
+  constexpr int CA = BM * BK / 8 / NTH, CB = BN * BK / 8 / NTH;  // 16-B chunks per thread per stage: 2, 2 (4)
+  constexpr int SLD = BN + 8;                    // epilogue staging row stride (floats)
+  constexpr int SMEM = NSTG * (BM + BN) * BK > BM * SLD * 2 ? NSTG * (BM + BN) * BK : BM * SLD * 2;  // + staging
+  __shared__ __attribute__((aligned(16))) bf16 smem[SMEM];  // 96 KB at 3 stages of 128 x 128, the only LDS object
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 2, wn = w & 3, r = lane & 31, h = lane >> 5;  // wave tile 64 x 32 at (64 wm, 32 wn)
+  const int wm = w >> 2, wn = w & 3, r = lane & 31, h = lane >> 5;  // wave tile 64 x WNC at (64 wm, WNC wn)
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM, nk = K / BK;
   const long T = (long)tiles_n * tiles_m * nk;
   const int G = gridDim.x, b = XM ? gemm3_vblock(blockIdx.x, G) : blockIdx.x;
@@ -1646,13 +1653,17 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
   // and the K position as the scalar offset (the host checks M * K and N * K bf16 fit 4 GB).  An LDS-DMA
   // instruction writes 64 consecutive 16-B slots (wave-uniform base + 16 lane), so the XOR swizzle is
   // applied on the global side: the lane filling slot s of row `row` fetches logical chunk s ^ f(row).
-  const __amdgpu_buffer_rsrc_t rx = attn_rsrc(X), rw = attn_rsrc(W);
+  // operand descriptors bounded to the operands (the host checks they fit 4 GB): an offset past them reads 0
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(X), (short)0,
+                                                                       (int)(uint32_t)((size_t)M * K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(W), (short)0,
+                                                                       (int)(uint32_t)((size_t)N * K * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rs = attn_rsrc(ep.sk_ws);
   auto slab_off = [&](int slab, int i, int j, int q) {
-    return (uint32_t)((((((size_t)slab * 8 + w) * 2 + i) * 4 + q) * 64 + lane) * 16);
+    return (uint32_t)(((((((size_t)slab * 8 + w) * 2 + i) * FJ + j) * 4 + q) * 64 + lane) * 16);
   };
   int* flag = reinterpret_cast<int*>(smem);
-  f32x16 acc[2][1];
+  f32x16 acc[2][FJ];
 
   for (long it = it_begin; it < it_end;) {
     const int t = (int)(it / nk), k0 = (int)(it - (long)t * nk);
@@ -1661,17 +1672,22 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
     const int m0 = tm * BM, n0 = tn * BN;
     const bool first_seg = it == it_begin;
     it += kn;
-    uint32_t oa[CA], ob[CB];
+    uint32_t oa[CA], ob[CB];  // CB = 2 CA at BN = 256: A and B offsets in separate loops
 #pragma unroll
     for (int i = 0; i < CA; i++) {
       const int c = i * NTH + w * 64 + lane, row = c >> 3, ch = (c & 7) ^ ((row >> 1) & 7);
       oa[i] = (uint32_t)(((size_t)min(m0 + row, M - 1) * K + (size_t)k0 * BK + ch * 8) * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < CB; i++) {
+      const int c = i * NTH + w * 64 + lane, row = c >> 3, ch = (c & 7) ^ ((row >> 1) & 7);
       ob[i] = (uint32_t)(((size_t)min(n0 + row, N - 1) * K + (size_t)k0 * BK + ch * 8) * 2);
     }
-    float bias[1], cscale[1];
+    static_assert(CA * NTH * 8 == BM * BK && CB * NTH * 8 == BN * BK, "every staged chunk has one lane");
+    float bias[FJ], cscale[FJ];
 #pragma unroll
-    for (int j = 0; j < 1; j++) {
-      const int n = min(n0 + wn * 32 + r, N - 1);
+    for (int j = 0; j < FJ; j++) {
+      const int n = min(n0 + wn * WNC + j * 32 + r, N - 1);
       bias[j] = to_f32(((const bf16*)ep.bias)[n]);
       cscale[j] = ep.col_scale ? ep.col_scale[n] : 1.f;
     }
@@ -1688,18 +1704,21 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
 #pragma unroll
     for (int i = 0; i < 2; i++)
 #pragma unroll
-      for (int j = 0; j < 1; j++)
+      for (int j = 0; j < FJ; j++)
 #pragma unroll
         for (int e = 0; e < 16; e++) acc[i][j][e] = 0.f;
     auto ktile = [&](int buf) {
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ks++) {
-        bf16x8 af[2], bfr[1];
+        bf16x8 af[2], bfr[FJ];
 #pragma unroll
         for (int i = 0; i < 2; i++) af[i] = *reinterpret_cast<const bf16x8*>(As(buf) + sw(wm * 64 + i * 32 + r, ks * 2 + h));
-        bfr[0] = *reinterpret_cast<const bf16x8*>(Bs(buf) + sw(wn * 32 + r, ks * 2 + h));
 #pragma unroll
-        for (int i = 0; i < 2; i++) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[0], acc[i][0], 0, 0, 0);
+        for (int j = 0; j < FJ; j++) bfr[j] = *reinterpret_cast<const bf16x8*>(Bs(buf) + sw(wn * WNC + j * 32 + r, ks * 2 + h));
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+          for (int j = 0; j < FJ; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     };
     // Step kt: this wave's DMA of tile kt retired (vmcnt(CA + CB) leaves tile kt + 1's in flight) ->
@@ -1735,7 +1754,7 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
 #pragma unroll
       for (int i = 0; i < 2; i++)
 #pragma unroll
-        for (int j = 0; j < 1; j++)
+        for (int j = 0; j < FJ; j++)
 #pragma unroll
           for (int q = 0; q < 4; q++) {
             const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
@@ -1758,7 +1777,7 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
 #pragma unroll
       for (int i = 0; i < 2; i++)
 #pragma unroll
-        for (int j = 0; j < 1; j++) {
+        for (int j = 0; j < FJ; j++) {
           f32x4 sum[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
           for (int bb = b_first; bb <= b_last; bb++) {
             const int sl = 2 * bb + (gemm3_first(bb, T, G) >= (long)t * nk ? 0 : 1);
@@ -1774,80 +1793,78 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
             for (int e = 0; e < 4; e++) acc[i][j][4 * q + e] = sum[q][e];
         }
     }
-    // Epilogue through LDS (the staging buffers are dead): each 64-row half of the tile is written there as
-    // fp32 (acc * col_scale + bias; row stride 136 floats, so the two lane halves of a store hit disjoint
-    // banks), then read back as 8-column chunks: one 16-B bf16 store (GELU, QKV) or two 16-B fp32 loads +
-    // stores (RESID) per chunk instead of 64 per-element accesses per lane.  The residual chunks and the
-    // rows' cached lengths of a half are loaded before its staging (clamped, unconditional: one round trip).
-    constexpr int SLD = 136;
+    // Epilogue through LDS (the staging buffers are dead): the whole tile is written there as fp32 (acc *
+    // col_scale + bias; row stride BN + 8 floats, so the two lane halves of a store hit disjoint banks; 68 KB of
+    // the 96 KB at BN = 128), one barrier, then read back as 8-column chunks: one 16-B bf16 store (GELU, QKV) or two 16-B fp32
+    // loads + stores (RESID) per chunk instead of 64 per-element accesses per lane.  The residual chunks and the
+    // rows' cached lengths are loaded before the staging (clamped, unconditional: one round trip).
+    constexpr int NCH = BM * BN / 8 / NTH, CPR = BN / 8;  // chunks per thread (4 or 8), chunks per row
     float* stg = reinterpret_cast<float*>(smem);
-    auto chunk_rc = [&](int half, int c, int& lr, int& lc) { const int id = tid + c * NTH; lr = half * 64 + (id >> 4); lc = (id & 15) * 8; };
+    auto chunk_rc = [&](int c, int& lr, int& lc) { const int id = tid + c * NTH; lr = id / CPR; lc = (id % CPR) * 8; };
+    f32x4 rsd[NCH][2];
+    int cpast[NCH];
 #pragma unroll
-    for (int half = 0; half < 2; half++) {
-      f32x4 rsd[2][2];
-      int cpast[2];
-#pragma unroll
-      for (int c = 0; c < 2; c++) {
-        int lr, lc;
-        chunk_rc(half, c, lr, lc);
-        const int m = min(m0 + lr, M - 1), n = min(n0 + lc, N - 8);
-        if constexpr (EK == EPI_RESID) {
-          rsd[c][0] = *reinterpret_cast<const f32x4*>(ep.resid + (size_t)m * ep.ldo + n);
-          rsd[c][1] = *reinterpret_cast<const f32x4*>(ep.resid + (size_t)m * ep.ldo + n + 4);
-        }
-        if constexpr (EK == EPI_QKV) cpast[c] = ep.past_dev ? ep.past_dev[m / ep.seq] : ep.past;
+    for (int c = 0; c < NCH; c++) {
+      int lr, lc;
+      chunk_rc(c, lr, lc);
+      const int m = min(m0 + lr, M - 1), n = min(n0 + lc, N - 8);
+      if constexpr (EK == EPI_RESID) {
+        rsd[c][0] = *reinterpret_cast<const f32x4*>(ep.resid + (size_t)m * ep.ldo + n);
+        rsd[c][1] = *reinterpret_cast<const f32x4*>(ep.resid + (size_t)m * ep.ldo + n + 4);
       }
-      if (wm == half) {
-#pragma unroll
-        for (int i = 0; i < 2; i++)
-#pragma unroll
-          for (int e = 0; e < 16; e++)
-            stg[(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * SLD + wn * 32 + r] = acc[i][0][e] * cscale[0] + bias[0];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int c = 0; c < 2; c++) {
-        int lr, lc;
-        chunk_rc(half, c, lr, lc);
-        const int m = m0 + lr, n = n0 + lc;
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + (lr - half * 64) * SLD + lc);
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + (lr - half * 64) * SLD + lc + 4);
-        if (m >= M || n >= N) continue;
-        if constexpr (EK == EPI_RESID) {
-          float* o = ep.out_f32 + (size_t)m * ep.ldo + n;
-          *reinterpret_cast<f32x4*>(o) = v0 + rsd[c][0];
-          *reinterpret_cast<f32x4*>(o + 4) = v1 + rsd[c][1];
-        } else {
-          bf16x8 b8;
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            b8[q] = from_f32<bf16>(EK == EPI_GELU ? gelu_bloom(v0[q]) : v0[q]);
-            b8[4 + q] = from_f32<bf16>(EK == EPI_GELU ? gelu_bloom(v1[q]) : v1[q]);
-          }
-          if constexpr (EK == EPI_GELU) {
-            *reinterpret_cast<bf16x8*>((bf16*)ep.out_act + (size_t)m * ep.ldo + n) = b8;
-          } else {
-            const int three = 3 * ep.head_dim;
-            const int head = n / three, rr = n - head * three, which = rr / ep.head_dim, d = rr - which * ep.head_dim;
-            bf16* dst;
-            if (which == 0) {
-              dst = (bf16*)ep.q_out + (size_t)m * ep.hidden + head * ep.head_dim + d;
-            } else {
-              const int bi = m / ep.seq, ti = m - bi * ep.seq;
-              dst = (bf16*)(which == 1 ? ep.k_cache : ep.v_cache) +
-                    (((size_t)(ep.slot + bi) * ep.n_head + head) * ep.max_ctx + cpast[c] + ti) * ep.head_dim + d;
-            }
-            *reinterpret_cast<bf16x8*>(dst) = b8;
-          }
-        }
-      }
-      __syncthreads();  // the staging rows are overwritten next (second half, or the next segment's tiles)
+      if constexpr (EK == EPI_QKV) cpast[c] = ep.past_dev ? ep.past_dev[m / ep.seq] : ep.past;
     }
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < FJ; j++)
+#pragma unroll
+        for (int e = 0; e < 16; e++)
+          stg[(wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * SLD + wn * WNC + j * 32 + r] = acc[i][j][e] * cscale[j] + bias[j];
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      int lr, lc;
+      chunk_rc(c, lr, lc);
+      const int m = m0 + lr, n = n0 + lc;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + lr * SLD + lc);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + lr * SLD + lc + 4);
+      if (m >= M || n >= N) continue;
+      if constexpr (EK == EPI_RESID) {
+        float* o = ep.out_f32 + (size_t)m * ep.ldo + n;
+        *reinterpret_cast<f32x4*>(o) = v0 + rsd[c][0];
+        *reinterpret_cast<f32x4*>(o + 4) = v1 + rsd[c][1];
+      } else {
+        bf16x8 b8;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          b8[q] = from_f32<bf16>(EK == EPI_GELU ? gelu_bloom(v0[q]) : v0[q]);
+          b8[4 + q] = from_f32<bf16>(EK == EPI_GELU ? gelu_bloom(v1[q]) : v1[q]);
+        }
+        if constexpr (EK == EPI_GELU) {
+          *reinterpret_cast<bf16x8*>((bf16*)ep.out_act + (size_t)m * ep.ldo + n) = b8;
+        } else {
+          const int three = 3 * ep.head_dim;
+          const int head = n / three, rr = n - head * three, which = rr / ep.head_dim, d = rr - which * ep.head_dim;
+          bf16* dst;
+          if (which == 0) {
+            dst = (bf16*)ep.q_out + (size_t)m * ep.hidden + head * ep.head_dim + d;
+          } else {
+            const int bi = m / ep.seq, ti = m - bi * ep.seq;
+            dst = (bf16*)(which == 1 ? ep.k_cache : ep.v_cache) +
+                  (((size_t)(ep.slot + bi) * ep.n_head + head) * ep.max_ctx + cpast[c] + ti) * ep.head_dim + d;
+          }
+          *reinterpret_cast<bf16x8*>(dst) = b8;
+        }
+      }
+    }
+    __syncthreads();  // the staging rows are overwritten next (the next segment's tiles)
   }
 #ifdef GEMM3_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();
   if (tid < 4 && b < 4096) g_gemm3_stamps[b * 4 + tid] = tid == 0 ? st0 : tid == 1 ? st1 : tid == 2 ? st2 : st3;
+#endif
 #endif
 }
 
@@ -1877,12 +1894,25 @@ static int gemm3_grid(int M, int N, int K, const Epi& ep) {
   return (int)G;
 }
 
-template <int NSTG = 3, bool XM = true>
+// Wide tiles (BN = 256): whole 128 x 256 tiles, one per block, when they fill 160..256 CUs with >= 32 K-steps each
+// (bloom-7b1 QKV / fc1 at 512 tokens: 192 / 256 tiles, where 128 x 128 tiles are 384 / 512 and stream-K splits
+// half of them; hipBLASLt picks one-tile-per-CU grids of wide tiles there too, profiles/r04_hipblaslt_kernels.txt).
+// G = tiles: every block's stream-K range is exactly one tile's K loop, so no partial tile, slab or ticket.
+static int gemm3_wide_grid(int M, int N, int K, const Epi& ep) {
+  if (K % 64 || N % 256 || ep.kind == EPI_ARGMAX) return 0;
+  if (ep.kind == EPI_QKV && ep.head_dim % 8) return 0;
+  if ((size_t)M * K * 2 >= (1ull << 32) || (size_t)N * K * 2 >= (1ull << 32)) return 0;
+  const long tiles = (long)((M + 127) / 128) * (N / 256);
+  if (tiles < 160 || tiles > 256 || K / 64 < 32) return 0;
+  return (int)tiles;
+}
+
+template <int NSTG = 3, bool XM = true, int BN = 128>
 static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int G) {
   switch (ep.kind) {
-    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, NSTG, XM><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
-    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, NSTG, XM><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
-    default: gemm_mfma3_kernel<EPI_GELU, NSTG, XM><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, NSTG, XM, BN><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, NSTG, XM, BN><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    default: gemm_mfma3_kernel<EPI_GELU, NSTG, XM, BN><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
   }
 }
 
@@ -2130,7 +2160,9 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
   if ((K % 64) == 0) {
     // 128x128 when it still gives every CU a block (>= 240 blocks), else 64x64, else 64x32
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-    if (const int g3 = gemm3_grid(M, N, K, ep)) {
+    if (const int gw = gemm3_wide_grid(M, N, K, ep)) {
+      gemm3_launch<3, true, 256>(x, w, M, N, K, ep, s, gw);
+    } else if (const int g3 = gemm3_grid(M, N, K, ep)) {
       gemm3_launch(x, w, M, N, K, ep, s, g3);
     } else if (blocks(128, 128) >= 240) {
       gemm2_launch<128, 128, 1>(x, w, M, N, K, ep, s);

@@ -154,3 +154,24 @@ def test_prefill512_multitile_causal_attention_wide_heads(h, nh):
     print(f"h={h} hd={h // nh}: prefill max-abs {err:.3e}, decode {err1:.3e}")
     gs.close()
     os_.close()
+
+
+@pytest.mark.parametrize("h,nh", [(4096, 32), (2560, 32)])
+def test_prefill512_one_row_wide_gemm_tiles(h, nh):
+    """One row x 512 tokens (M = 512): the prefill GEMMs whose 128 x 256 tiles fill 160..256 CUs take the wide-tile
+    gemm_mfma3 (bloom-7b1 QKV 192 tiles and fc1 256 tiles; bloom-3b fc1 160 tiles), one whole tile per block;
+    hidden states and the next decode step against the checker."""
+    B, S, V = 1, 512, 1024
+    gs = Stage(h, nh, 1, V, 0, 1, dtype="bf16", max_batch=B, max_ctx=S + 1, max_tokens=B * S, seed=67,
+               is_last=False)
+    os_ = OracleStage(h, nh, 1, V, 0, 1, bf16=True, max_batch=B, max_ctx=S + 1, seed=67, is_last=False)
+    ids = gen_np.prompt_ids(71, B, S + 1, V).astype(np.int32)
+    out_g = gs.forward_host(ids[:, :S], B, S, past_len=0)
+    out_o = os_.forward(ids[:, :S], B, S, past_len=0)
+    err = check_close(out_g, out_o, "bf16", f"h={h} wide-tile prefill {B}x{S}")
+    d_g = gs.forward_host(ids[:, S:S + 1], B, 1, past_len=S)
+    d_o = os_.forward(ids[:, S:S + 1], B, 1, past_len=S)
+    err1 = check_close(d_g, d_o, "bf16", f"h={h} decode after the wide-tile prefill")
+    print(f"h={h}: wide-tile prefill max-abs {err:.3e}, decode {err1:.3e}")
+    gs.close()
+    os_.close()

@@ -94,6 +94,16 @@ int main() {
         if (md > 1e-3) printf("           MISMATCH max |diff| %.3g\n", md);
       }
     }
+    if (const int gw = gemm3_wide_grid(M, N, K, ep)) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "m32 wide 128x256 G=%d", gw);
+      const float us = timeit([&] { gemm3_launch<3, true, 256>(X, W, M, N, K, ep, 0, gw); });
+      CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (size_t i = 0; i < ho.size(); i++) md = std::max(md, (double)fabsf(ho[i] - hr[i]));
+      line(nm, us);
+      if (md > 1e-3) printf("           MISMATCH max |diff| %.3g\n", md);
+    }
     for (int v = 0; v < 6; v++) {
       const int G = v < 3 ? (int[]){192, 256, 384}[v] : (int[]){256, 384, 512}[v - 3];
       const int nst = v < 3 ? 3 : 2;
