@@ -2439,12 +2439,12 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(AttnArgs a) {
 // Prefill (S > 1), bf16: MFMA flash attention.  Block = (64-query tile, head, row b), 4 waves x 16
 // queries.  Per 64-key tile: K rows and V^T staged in LDS by the block, the NEXT tile's K/V rows
 // already in flight to registers while this one computes (the loop was load-latency bound: one
-// HBM round trip per 32-key tile, 39 us per bloom-1b1 layer at S = 512); S = Q.K^T on
-// v_mfma_f32_16x16x32_bf16 (Q fragments in registers, zero-padded past hd); scale + ALiBi + causal
-// mask + online softmax on the accumulator layout (row = 4*(lane>>4)+i, key = lane&15; row
-// reductions by DPP inside the 16-lane row); P -> fp16 through LDS into the A operand of the P.V
-// MFMAs (v_mfma_f32_16x16x32_f16; V is staged as fp16 — exact for bf16 values in fp16's normal
-// range).  P is split into fp16(p) + fp16(p - fp16(p)) and both halves run through the P.V MFMAs,
+// HBM round trip per 32-key tile, 39 us per bloom-1b1 layer at S = 512); S^T = K.Q^T on
+// v_mfma_f32_16x16x32_bf16 (Q fragments in registers, zero-padded past hd), so a lane holds ONE query
+// against 16 keys: scale + ALiBi + causal mask + online softmax per lane with two cross-lane steps per
+// reduction, and the lane's P values are already the A-operand elements of the P.V MFMAs
+// (v_mfma_f32_16x16x32_f16) once V^T is staged in the matching key order (round 4: no P round trip
+// through LDS); V is staged as fp16 — exact for bf16 values in fp16's normal range.  P is split into fp16(p) + fp16(p - fp16(p)) and both halves run through the P.V MFMAs,
 // so P keeps ~21 bits like the fp32 P of the checker (one fp16 P alone moved bloom-1b1's 512-token
 // prefill logits 2.06e-2 off the bf16-mode checker).  q is bf16 (the stage stores q in the
 // activation dtype); accumulation and softmax fp32.  The heaviest query tiles (most keys under
@@ -2459,8 +2459,6 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   constexpr int CPT = (KT * HDP / 8 + 255) / 256;  // 16-B K (and V) chunks per thread per tile
   __shared__ __attribute__((aligned(16))) bf16 Ks[KT * KLD];
   __shared__ __attribute__((aligned(16))) _Float16 Vt[HDP * VLD];
-  __shared__ __attribute__((aligned(16))) _Float16 Ps[4][16 * VLD];
-  __shared__ __attribute__((aligned(16))) _Float16 Pl[4][16 * VLD];  // p - fp16(p): P keeps ~21 bits
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
   // split-KV (a.pf_tiles > 0): blockIdx.x = (query tile, key split); heaviest query tiles first
   const int nspl = gridDim.x / ((a.S + 63) / 64);
@@ -2485,10 +2483,8 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   const bf16* kb = (const bf16*)a.k_cache + rowbase * hd;
   const bf16* vb = (const bf16*)a.v_cache + rowbase * hd;
   const float slope = a.slopes[head];
-  float m_run[4], l_run[4];
+  float m_q = -INFINITY, l_q = 0.f;  // running max / sum of query q0 + r (the 4 lanes r + 16 g agree)
   f32x4 o[NT];
-#pragma unroll
-  for (int i = 0; i < 4; i++) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
 #pragma unroll
   for (int t = 0; t < NT; t++) o[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   // keys visible to the block's last query; a split takes key tiles [spl * pf_tiles, + pf_tiles)
@@ -2507,6 +2503,9 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   // V^T row d keeps its 8-key chunks XOR-swizzled by (d >> 3): the transposing element stores of a
   // wave (lanes = 8-dim slices of a few keys) then spread over the LDS banks instead of two
   auto vsw = [](int d, int key) { return d * VLD + ((((key >> 3) ^ (d >> 3)) & 7) << 3) + (key & 7); };
+  // V^T keys are stored in the order the P fragments come out of the S^T accumulators: in each 32-key block,
+  // key 16 h + 4 g + j sits at 8 g + 4 h + j, so lane group g's 8 k-elements of a P.V step are contiguous
+  auto kperm = [](int k) { return (k & ~31) | (((k >> 2) & 3) << 3) | (((k >> 4) & 1) << 2) | (k & 3); };
   // V is staged by (4 keys x 8 dims) items: one 8-B LDS store per dim writes 4 keys of V^T
   // (a thread per item; KT/4 * hd/8 <= 256 items)
   const int nvi = (KT / 4) * nchunk;
@@ -2552,12 +2551,14 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       for (int j = 0; j < 8; j++) {
         const f16x4 v4 = {ok0 ? (_Float16)(float)vreg[0][j] : (_Float16)0.f, ok1 ? (_Float16)(float)vreg[1][j] : (_Float16)0.f,
                           ok2 ? (_Float16)(float)vreg[2][j] : (_Float16)0.f, ok3 ? (_Float16)(float)vreg[3][j] : (_Float16)0.f};
-        *reinterpret_cast<f16x4*>(&Vt[vsw(vdc + j, vq * 4)]) = v4;
+        *reinterpret_cast<f16x4*>(&Vt[vsw(vdc + j, kperm(vq * 4))]) = v4;
       }
     }
     __syncthreads();
     if (k0 + KT < kstop) gload(k0 + KT, kend - 1);  // next tile in flight while this one computes
-    // S tiles: four 16-key tiles
+    // S^T tiles: four 16-key tiles, K as the A operand and Q as B, so lane (r, g) holds query q0 + r against keys
+    // t*16 + 4g + i: a query's softmax statistics need two cross-lane steps (xor 16, xor 32) instead of four DPP
+    // steps per row, and its P values feed the P.V A operand straight from registers (no LDS round trip)
     f32x4 sacc[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
@@ -2565,77 +2566,77 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
 #pragma unroll
       for (int ks = 0; ks < KS; ks++) {
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(t * 16 + r) * KLD + ks * 32 + 8 * g]);
-        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, sacc[t], 0, 0, 0);
+        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], sacc[t], 0, 0, 0);
       }
     }
-    // scale, ALiBi, causal mask; lane holds rows 4g+i, key t*16 + r
-    float sv[4][4], rmax[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int qpos = past + q0 + 4 * g + i;
-      rmax[i] = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < 4; t++) {
-        const int kpos = k0 + t * 16 + r;
-        const float v = (kpos <= qpos && kpos < kstop) ? slope * (float)kpos + a.inv_norm * sacc[t][i] : -INFINITY;
-        sv[t][i] = v;
-        rmax[i] = fmaxf(rmax[i], v);
-      }
-      rmax[i] = fmaxf(rmax[i], dpp_f<0xB1>(rmax[i]));  // max over the 16 lanes of the row
-      rmax[i] = fmaxf(rmax[i], dpp_f<0x4E>(rmax[i]));
-      rmax[i] = fmaxf(rmax[i], dpp_f<0x124>(rmax[i]));
-      rmax[i] = fmaxf(rmax[i], dpp_f<0x128>(rmax[i]));
-    }
-    float scale[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const float m_new = fmaxf(m_run[i], rmax[i]);
-      // rows whose keys are all masked so far keep m = -inf; exp(-inf - -inf) guarded
-      scale[i] = m_new == -INFINITY ? 1.f : __expf(m_run[i] - m_new);
-      float rs = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; t++) {
-        const float p = m_new == -INFINITY ? 0.f : __expf(sv[t][i] - m_new);
-        sv[t][i] = p;
-        rs += p;
-      }
-      rs += dpp_f<0xB1>(rs);
-      rs += dpp_f<0x4E>(rs);
-      rs += dpp_f<0x124>(rs);
-      rs += dpp_f<0x128>(rs);
-      l_run[i] = l_run[i] * scale[i] + rs;
-      m_run[i] = m_new;
-    }
-#pragma unroll
-    for (int t = 0; t < NT; t++)
-#pragma unroll
-      for (int i = 0; i < 4; i++) o[t][i] *= scale[i];
-    // P -> LDS (fp16, [16 q][64 keys]) -> A fragments
+    // scale, ALiBi, causal mask
+    const int qpos = past + q0 + r;
+    float sv[4][4], rmax = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 4; t++)
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        const _Float16 hi = (_Float16)sv[t][i];
-        Ps[w][(4 * g + i) * VLD + t * 16 + r] = hi;
-        Pl[w][(4 * g + i) * VLD + t * 16 + r] = (_Float16)(sv[t][i] - (float)hi);
+        const int kpos = k0 + t * 16 + 4 * g + i;
+        const float v = (kpos <= qpos && kpos < kstop) ? slope * (float)kpos + a.inv_norm * sacc[t][i] : -INFINITY;
+        sv[t][i] = v;
+        rmax = fmaxf(rmax, v);
       }
-    __builtin_amdgcn_wave_barrier();
+    rmax = fmaxf(rmax, __shfl_xor(rmax, 16, 64));
+    rmax = fmaxf(rmax, __shfl_xor(rmax, 32, 64));
+    const float m_new = fmaxf(m_q, rmax);
+    // queries whose keys are all masked so far keep m = -inf; exp(-inf - -inf) guarded
+    const float scale_q = m_new == -INFINITY ? 1.f : __expf(m_q - m_new);
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const float p = m_new == -INFINITY ? 0.f : __expf(sv[t][i] - m_new);
+        sv[t][i] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l_q = l_q * scale_q + rs;
+    m_q = m_new;
+    // the output accumulators hold queries 4g + i: their scales come from lanes 4g + i
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const float sc = __shfl(scale_q, 4 * g + i, 64);
+#pragma unroll
+      for (int t = 0; t < NT; t++) o[t][i] *= sc;
+    }
+    // P fragments of the two 32-key steps: keys 32 kb + 16 h + 4 g + j (h, j < 2, 4) = tiles 2 kb + h, element j;
+    // P = fp16(p) + fp16(p - fp16(p)) (~21 bits)
     typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-    const f16x8 pf0 = *reinterpret_cast<const f16x8*>(&Ps[w][r * VLD + 8 * g]);
-    const f16x8 pf1 = *reinterpret_cast<const f16x8*>(&Ps[w][r * VLD + 32 + 8 * g]);
-    const f16x8 pl0 = *reinterpret_cast<const f16x8*>(&Pl[w][r * VLD + 8 * g]);
-    const f16x8 pl1 = *reinterpret_cast<const f16x8*>(&Pl[w][r * VLD + 32 + 8 * g]);
+    f16x8 pf[2], pl[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const float p = sv[2 * kb + (e >> 2)][e & 3];
+        const _Float16 hi = (_Float16)p;
+        pf[kb][e] = hi;
+        pl[kb][e] = (_Float16)(p - (float)hi);
+      }
 #pragma unroll
     for (int t = 0; t < NT; t++) {
       const f16x8 vf0 = *reinterpret_cast<const f16x8*>(&Vt[vsw(t * 16 + r, 8 * g)]);
       const f16x8 vf1 = *reinterpret_cast<const f16x8*>(&Vt[vsw(t * 16 + r, 32 + 8 * g)]);
-      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf0, vf0, o[t], 0, 0, 0);
-      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf1, vf1, o[t], 0, 0, 0);
+      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf[0], vf0, o[t], 0, 0, 0);
+      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf[1], vf1, o[t], 0, 0, 0);
       if constexpr (PLO) {
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl0, vf0, o[t], 0, 0, 0);
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl1, vf1, o[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl[0], vf0, o[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl[1], vf1, o[t], 0, 0, 0);
       }
     }
+  }
+  // the statistics of the accumulator rows (queries q0 + 4g + i)
+  float m_run[4], l_run[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    m_run[i] = __shfl(m_q, 4 * g + i, 64);
+    l_run[i] = __shfl(l_q, 4 * g + i, 64);
   }
   if (nspl > 1) {
     // split partial (running max, sum, unnormalised context) of the block's 64 queries, write-through:
@@ -2752,6 +2753,8 @@ size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, 
 // merge knows it without a device round trip.
 // A wide variant (2-wave blocks of 32 positions, one block per 64 cached positions, ticket merge in the
 // launch) measured bloom-7b1 B = 1 +1.7 %, bloom-1b1 B = 1 -4 % (profiles/r02_attn_wide_ab.txt): removed.
+// Round 4 A/B (profiles/r04_attn_decode_splits_ab.txt): 2 or 1 chunks per split instead of 4 -- more blocks
+// streaming the cache, more partials for the dense prologue to merge -- cost bloom-1b1 B = 1 3 %.
 int attention_decode_splits(int B, int n_head, int max_chunks) {
   const int pairs = B * n_head;
   if (pairs >= 192 || max_chunks <= 4) return 1;
