@@ -1907,6 +1907,22 @@ static int gemm3_wide_grid(int M, int N, int K, const Epi& ep) {
   return (int)tiles;
 }
 
+// Two blocks per CU (2 LDS stages, 68 KB each) on whole tiles: when the 128 x 128 tiles number >= 512 and split
+// evenly over 512 (or 384) blocks, every block runs whole tiles (no partial tile) and a second block per CU
+// covers the first one's barriers and epilogue: bloom-7b1 QKV at 2048 tokens 257 -> 233 us, fc1 at 1024 tokens
+// 175 -> 154 us, bloom-1b1 QKV at 4096 tokens (1152 tiles, 384 blocks) 109 -> 98 us
+// (profiles/r04_gemm_long_prompts.txt).
+static int gemm3_pair_grid(int M, int N, int K, const Epi& ep) {
+  if (K % 64 || N % 8 || ep.kind == EPI_ARGMAX || K / 64 < 16) return 0;
+  if (ep.kind == EPI_QKV && ep.head_dim % 8) return 0;
+  if ((size_t)M * K * 2 >= (1ull << 32) || (size_t)N * K * 2 >= (1ull << 32)) return 0;
+  const long tiles = (long)((M + 127) / 128) * ((N + 127) / 128);
+  if (tiles < 512) return 0;
+  if (tiles % 512 == 0) return 512;
+  if (tiles % 384 == 0) return 384;
+  return 0;
+}
+
 template <int NSTG = 3, bool XM = true, int BN = 128>
 static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int G) {
   switch (ep.kind) {
@@ -2162,6 +2178,8 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
     if (const int gw = gemm3_wide_grid(M, N, K, ep)) {
       gemm3_launch<3, true, 256>(x, w, M, N, K, ep, s, gw);
+    } else if (const int gp = gemm3_pair_grid(M, N, K, ep)) {
+      gemm3_launch<2>(x, w, M, N, K, ep, s, gp);
     } else if (const int g3 = gemm3_grid(M, N, K, ep)) {
       gemm3_launch(x, w, M, N, K, ep, s, g3);
     } else if (blocks(128, 128) >= 240) {

@@ -23,14 +23,18 @@ int main() {
   struct Sh { const char* name; int M, N, K; } shapes[] = {
       {"1b1 qkv", 512, 4608, 1536}, {"1b1 dense", 512, 1536, 1536}, {"1b1 fc1", 512, 6144, 1536},
       {"1b1 fc2", 512, 1536, 6144}, {"7b1 qkv", 512, 12288, 4096}, {"7b1 dense", 512, 4096, 4096},
-      {"7b1 fc1", 512, 16384, 4096}, {"7b1 fc2", 512, 4096, 16384}, {"3b dense B2", 1024, 2560, 2560}};
+      {"7b1 fc1", 512, 16384, 4096}, {"7b1 fc2", 512, 4096, 16384}, {"3b dense B2", 1024, 2560, 2560},
+      // long prompts / batched prefill: >= 512 tiles (the 2-stage, two-blocks-per-CU question)
+      {"7b1 qkv 2k", 2048, 12288, 4096}, {"7b1 fc1 1k", 1024, 16384, 4096}, {"7b1 dense 2k", 2048, 4096, 4096},
+      {"1b1 fc1 4k", 4096, 6144, 1536}, {"1b1 qkv 4k", 4096, 4608, 1536}};
   bf16 *X, *W, *bias; float *out, *ref, *resid, *ws; unsigned* tick;
-  CK(hipMalloc(&X, (size_t)1024 * 16384 * 2)); CK(hipMalloc(&W, (size_t)16384 * 16384 * 2));
-  CK(hipMalloc(&bias, 65536 * 2)); CK(hipMalloc(&out, (size_t)1024 * 16384 * 4)); CK(hipMalloc(&ref, (size_t)1024 * 16384 * 4));
-  CK(hipMalloc(&resid, (size_t)1024 * 16384 * 4)); CK(hipMemset(resid, 0, (size_t)1024 * 16384 * 4));
+  const size_t MMAX = 4096;
+  CK(hipMalloc(&X, MMAX * 16384 * 2)); CK(hipMalloc(&W, (size_t)16384 * 16384 * 2));
+  CK(hipMalloc(&bias, 65536 * 2)); CK(hipMalloc(&out, MMAX * 16384 * 4)); CK(hipMalloc(&ref, MMAX * 16384 * 4));
+  CK(hipMalloc(&resid, MMAX * 16384 * 4)); CK(hipMemset(resid, 0, MMAX * 16384 * 4));
   const size_t cap = (size_t)1024 * 128 * 128;
   CK(hipMalloc(&ws, cap * 4)); CK(hipMalloc(&tick, 4096 * 4)); CK(hipMemset(tick, 0, 4096 * 4));
-  fill_rand<<<4096, 256>>>(X, (size_t)1024 * 16384, 1); fill_rand<<<4096, 256>>>(W, (size_t)16384 * 16384, 2);
+  fill_rand<<<4096, 256>>>(X, MMAX * 16384, 1); fill_rand<<<4096, 256>>>(W, (size_t)16384 * 16384, 2);
   fill_rand<<<64, 256>>>(bias, 65536, 3);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
