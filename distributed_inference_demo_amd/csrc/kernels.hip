@@ -556,17 +556,60 @@ __device__ __forceinline__ void ln_rows_finish(const LnArgs& ln, int M, int K, f
   __syncthreads();
 }
 
-// LayerNorm of M fp32 rows (K <= 4096, K % 4 == 0) -> bf16, one 256-thread block per row, the row
-// held in registers (one global pass, one block reduction): the producer of a batched GEMV's input.
-__global__ __launch_bounds__(256) void ln_rows_kernel(LnArgs ln, int K, bf16* __restrict__ out) {
-  __shared__ float scratch[64];
-  LnArgs lr = ln;
-  lr.x = ln.x + (size_t)blockIdx.x * ln.row_stride * K;
-  float4 xv[1][4];
-  float c[1];
-  uint2 gb[4][2];
-  ln_rows_load<1>(lr, 1, K, xv, c, gb);
-  ln_rows_finish<1>(lr, 1, K, xv, c, gb, out + (size_t)blockIdx.x * K, scratch);
+// LayerNorm of M fp32 rows (K <= 4096, K % 4 == 0) -> bf16 with ONE WAVE per row (a 64-thread block): the row in
+// registers (NV float4 per lane), the shifted-sum statistics of ln_rows_finish by DPP wave reductions -- no LDS
+// and no barrier (round 4; the 256-thread block per row paid two block barriers for 6 KB of row).
+template <int NV>
+__global__ __launch_bounds__(64) void ln_rows_wave_kernel(LnArgs ln, int K, bf16* __restrict__ out) {
+  const int lane = threadIdx.x;
+  const float* xr = ln.x + (size_t)blockIdx.x * ln.row_stride * K + (size_t)ln.row_offset * K;
+  float4 xv[NV];
+  uint2 gr[NV], br[NV];
+  const float c = xr[0];
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    const int k = (i * 64 + lane) * 4;
+    xv[i] = k < K ? *reinterpret_cast<const float4*>(xr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gr[i] = k < K ? *reinterpret_cast<const uint2*>(ln.gamma + k) : make_uint2(0u, 0u);
+    br[i] = k < K ? *reinterpret_cast<const uint2*>(ln.beta + k) : make_uint2(0u, 0u);
+  }
+  float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    if ((i * 64 + lane) * 4 < K) {
+      const float d0 = xv[i].x - c, d1 = xv[i].y - c, d2 = xv[i].z - c, d3 = xv[i].w - c;
+      a1 += (d0 + d1) + (d2 + d3);
+      a2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    }
+  }
+  const float invk = 1.0f / (float)K;
+  const float t1 = wave_sum(a1) * invk, t2 = wave_sum(a2) * invk;
+  const float mean = c + t1, rstd = 1.0f / sqrtf(fmaxf(t2 - t1 * t1, 0.f) + ln.eps);
+  bf16* orow = out + (size_t)blockIdx.x * K;
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    const int k = (i * 64 + lane) * 4;
+    if (k < K) {
+      float4 g, b;
+      bf16x4_to_f32(gr[i], g);
+      bf16x4_to_f32(br[i], b);
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 o;
+      o[0] = (bf16)((xv[i].x - mean) * rstd * g.x + b.x);
+      o[1] = (bf16)((xv[i].y - mean) * rstd * g.y + b.y);
+      o[2] = (bf16)((xv[i].z - mean) * rstd * g.z + b.z);
+      o[3] = (bf16)((xv[i].w - mean) * rstd * g.w + b.w);
+      *reinterpret_cast<bf16x4*>(orow + k) = o;
+    }
+  }
+}
+
+// K <= 4096, K % 4 == 0: one wave per row, NV = ceil(K / 256) float4 per lane.
+static void launch_ln_rows_wave(const LnArgs& ln, int M, int K, bf16* out, hipStream_t s) {
+  const int nv = (K + 255) / 256;
+  if (nv <= 4) ln_rows_wave_kernel<4><<<M, 64, 0, s>>>(ln, K, out);
+  else if (nv <= 8) ln_rows_wave_kernel<8><<<M, 64, 0, s>>>(ln, K, out);
+  else ln_rows_wave_kernel<16><<<M, 64, 0, s>>>(ln, K, out);
 }
 
 // Diagnostic builds only (tools/gemv_timeline.hip defines BS_STAMPS): wave 0 of every block records
@@ -2117,7 +2160,7 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
   }
   if (is_bf16 && K <= 4096 && (K % 4) == 0) {
     LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
-    ln_rows_kernel<<<M, 256, 0, s>>>(ln, K, (bf16*)xn_scratch);
+    launch_ln_rows_wave(ln, M, K, (bf16*)xn_scratch, s);
   } else {
     launch_layernorm(is_bf16, x, nullptr, row_stride, row_offset, gamma, beta, xn_scratch, 0, M, K, eps, s);
   }
@@ -3331,7 +3374,7 @@ void launch_ln_rows(const float* x, int row_stride, int row_offset, const void* 
                     void* out_bf16, int M, int K, hipStream_t s) {
   if (K <= 4096 && (K % 4) == 0) {
     LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
-    ln_rows_kernel<<<M, 256, 0, s>>>(ln, K, (bf16*)out_bf16);
+    launch_ln_rows_wave(ln, M, K, (bf16*)out_bf16, s);
   } else {
     launch_layernorm(1, x, nullptr, row_stride, row_offset, gamma, beta, out_bf16, 0, M, K, eps, s);
   }

@@ -57,7 +57,7 @@ def test_ldsw4_ragged_tile_columns(B):
 
 @pytest.mark.parametrize("B", [8, 32])
 def test_batched_decode_middle_stage_offset_rows(B):
-    """4 < B <= 32 (ln_rows_kernel + gemv_ldsw4): a 3-layer bloom-1b1-width middle stage fed hidden states
+    """4 < B <= 32 (ln_rows_wave_kernel + gemv_ldsw4): a 3-layer bloom-1b1-width middle stage fed hidden states
     with a large common offset (|mean| 20 x std: a plain one-pass sum-of-squares variance would cancel; the
     kernel's shifted sums must not) decodes 3 steps; every output within the wide-block bound."""
     h, nh, L, V = 1536, 16, 4, 2048

@@ -170,7 +170,7 @@ int main() {
           }
         }});
         vars.push_back({"tiles (+ln_rows)", [&](const bf16* w) {
-          if (sh.ln) ln_rows_kernel<<<M, 256>>>(ln, K, xn);
+          if (sh.ln) launch_ln_rows_wave(ln, M, K, xn, 0);
           gemv_tiles_dispatch(xn, w, M, N, K, eps, 0);
         }});
         if (sh.ln) vars.push_back({"tiles (no LN)", [&](const bf16* w) { gemv_tiles_dispatch(xn, w, M, N, K, eps, 0); }});
