@@ -2510,24 +2510,28 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(AttnArgs a) {
 // prefill logits 2.06e-2 off the bf16-mode checker).  q is bf16 (the stage stores q in the
 // activation dtype); accumulation and softmax fp32.  The heaviest query tiles (most keys under
 // the causal mask) are dispatched first.
-template <int HDP, bool PLO = true>  // head_dim padded to a multiple of 32 (64, 96, 128); PLO: P hi + lo
-__global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
+// QW waves per block = QW x 16 queries (4: 64-query tiles; 2: 32-query tiles, twice the blocks).
+template <int HDP, bool PLO = true, int QW = 4>  // head_dim padded to a multiple of 32 (64, 96, 128); PLO: P hi + lo
+__global__ __launch_bounds__(QW * 64) void attn_prefill_mfma_kernel(AttnArgs a) {
   constexpr int KT = 64;                 // keys per tile
+  constexpr int QB = QW * 16;            // queries per block
+  constexpr int NTH = QW * 64;
   constexpr int KS = HDP / 32;           // k-steps of S = Q.K^T
   constexpr int NT = HDP / 16;           // 16-dim output tiles
   constexpr int KLD = HDP + 8;           // padded K row (bf16 elements)
   constexpr int VLD = KT + 8;            // padded V^T row
-  constexpr int CPT = (KT * HDP / 8 + 255) / 256;  // 16-B K (and V) chunks per thread per tile
+  constexpr int CPT = (KT * HDP / 8 + NTH - 1) / NTH;  // 16-B K chunks per thread per tile
+  constexpr int VPT = (KT / 4 * HDP / 8 + NTH - 1) / NTH;  // V staging items per thread (4 keys x 8 dims)
   __shared__ __attribute__((aligned(16))) bf16 Ks[KT * KLD];
   __shared__ __attribute__((aligned(16))) _Float16 Vt[HDP * VLD];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
   // split-KV (a.pf_tiles > 0): blockIdx.x = (query tile, key split); heaviest query tiles first
-  const int nspl = gridDim.x / ((a.S + 63) / 64);
+  const int nspl = gridDim.x / ((a.S + QB - 1) / QB);
   const int qt = (gridDim.x - 1 - blockIdx.x) / nspl, spl = (gridDim.x - 1 - blockIdx.x) % nspl;
   const int head = blockIdx.y, b = blockIdx.z;
   const int hd = a.head_dim;
   const int past = a.past_dev ? a.past_dev[b] : a.past;
-  const int q0 = qt * 64 + w * 16;          // first query (within this call) of the wave
+  const int q0 = qt * QB + w * 16;          // first query (within this call) of the wave
   const bf16* qg = (const bf16*)a.q;
   // Q fragments: lane holds Q[q0 + r][ks*32 + 8g .. +8]
   bf16x8 qf[KS];
@@ -2549,13 +2553,13 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < NT; t++) o[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   // keys visible to the block's last query; a split takes key tiles [spl * pf_tiles, + pf_tiles)
-  const int kend = past + min(a.S, qt * 64 + 64);
+  const int kend = past + min(a.S, qt * QB + QB);
   const int kbeg = nspl > 1 ? min(spl * a.pf_tiles * KT, kend) : 0;
   const int kstop = nspl > 1 ? min(kbeg + a.pf_tiles * KT, kend) : kend;
   const int nchunk = hd / 8, nch = KT * nchunk;
   // the padded dims are never staged: zero them once (keeps the MFMA inputs finite)
   if (HDP != 0) {
-    for (int c = tid; c < KT * (HDP - hd); c += 256) {
+    for (int c = tid; c < KT * (HDP - hd); c += NTH) {
       const int kr = c / (HDP - hd), d = hd + (c - kr * (HDP - hd));
       Ks[kr * KLD + d] = (bf16)0.f;
       Vt[d * VLD + kr] = (_Float16)0.f;
@@ -2568,25 +2572,33 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
   // key 16 h + 4 g + j sits at 8 g + 4 h + j, so lane group g's 8 k-elements of a P.V step are contiguous
   auto kperm = [](int k) { return (k & ~31) | (((k >> 2) & 3) << 3) | (((k >> 4) & 1) << 2) | (k & 3); };
   // V is staged by (4 keys x 8 dims) items: one 8-B LDS store per dim writes 4 keys of V^T
-  // (a thread per item; KT/4 * hd/8 <= 256 items)
+  // (VPT items per thread; KT/4 * hd/8 <= 256 items)
   const int nvi = (KT / 4) * nchunk;
-  const int vq = min(tid, nvi - 1) / nchunk, vdc = (min(tid, nvi - 1) % nchunk) * 8;
+  int vq[VPT], vdc[VPT];
+#pragma unroll
+  for (int v = 0; v < VPT; v++) {
+    const int it = min(tid + v * NTH, nvi - 1);
+    vq[v] = it / nchunk;
+    vdc[v] = (it % nchunk) * 8;
+  }
   // one register stage: tile k0 + KT is in flight while tile k0 computes (a second stage, tile k0 + 2 KT,
   // measured no faster: profiles/r03_attn_prefill_split.txt)
-  bf16x8 kreg[CPT], vreg[4];
+  bf16x8 kreg[CPT], vreg[VPT][4];
   auto gload = [&](int k0, int lim) {  // clamped to key lim: loads past it re-read that key
 #pragma unroll
     for (int i = 0; i < CPT; i++) {
-      const int c = min(tid + i * 256, nch - 1);
+      const int c = min(tid + i * NTH, nch - 1);
       const int kr = c / nchunk, dc = (c - kr * nchunk) * 8;
       const int key = min(k0 + kr, lim);
       kreg[i] = *reinterpret_cast<const bf16x8*>(kb + (size_t)key * hd + dc);
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int key = min(k0 + vq * 4 + i, lim);
-      vreg[i] = *reinterpret_cast<const bf16x8*>(vb + (size_t)key * hd + vdc);
-    }
+    for (int v = 0; v < VPT; v++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int key = min(k0 + vq[v] * 4 + i, lim);
+        vreg[v][i] = *reinterpret_cast<const bf16x8*>(vb + (size_t)key * hd + vdc[v]);
+      }
   };
   // The first tile is requested at the split's nominal start, clamped to the cache rather than to the
   // context, so it does not wait for past_len: keys past the context are masked (p = 0) and their V is
@@ -2596,23 +2608,26 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
     __syncthreads();  // previous tile's LDS reads are done
 #pragma unroll
     for (int i = 0; i < CPT; i++) {
-      const int c = tid + i * 256;
+      const int c = tid + i * NTH;
       if (c < nch) {
         const int kr = c / nchunk, dc = (c - kr * nchunk) * 8;
         *reinterpret_cast<bf16x8*>(&Ks[kr * KLD + dc]) = kreg[i];
       }
     }
-    if (tid < nvi) {
-      typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-      // keys past the split's end are staged as 0: their p is 0, but a stale cache row there (an earlier
-      // request's, past this one's context) could hold a value outside fp16's range, and 0 * inf is NaN
-      const int kv0 = k0 + vq * 4;
-      const bool ok0 = kv0 < kstop, ok1 = kv0 + 1 < kstop, ok2 = kv0 + 2 < kstop, ok3 = kv0 + 3 < kstop;
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const f16x4 v4 = {ok0 ? (_Float16)(float)vreg[0][j] : (_Float16)0.f, ok1 ? (_Float16)(float)vreg[1][j] : (_Float16)0.f,
-                          ok2 ? (_Float16)(float)vreg[2][j] : (_Float16)0.f, ok3 ? (_Float16)(float)vreg[3][j] : (_Float16)0.f};
-        *reinterpret_cast<f16x4*>(&Vt[vsw(vdc + j, kperm(vq * 4))]) = v4;
+    for (int v = 0; v < VPT; v++) {
+      if (tid + v * NTH < nvi) {
+        typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+        // keys past the split's end are staged as 0: their p is 0, but a stale cache row there (an earlier
+        // request's, past this one's context) could hold a value outside fp16's range, and 0 * inf is NaN
+        const int kv0 = k0 + vq[v] * 4;
+        const bool ok0 = kv0 < kstop, ok1 = kv0 + 1 < kstop, ok2 = kv0 + 2 < kstop, ok3 = kv0 + 3 < kstop;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const f16x4 v4 = {ok0 ? (_Float16)(float)vreg[v][0][j] : (_Float16)0.f, ok1 ? (_Float16)(float)vreg[v][1][j] : (_Float16)0.f,
+                            ok2 ? (_Float16)(float)vreg[v][2][j] : (_Float16)0.f, ok3 ? (_Float16)(float)vreg[v][3][j] : (_Float16)0.f};
+          *reinterpret_cast<f16x4*>(&Vt[vsw(vdc[v] + j, kperm(vq[v] * 4))]) = v4;
+        }
       }
     }
     __syncthreads();
@@ -2704,12 +2719,12 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
     // record [m, l, -, -, o[0..hd)] per (split, query); the block drawing the last ticket of its (row,
     // head, query tile) merges the splits in split order
     const int rs = hd + 4;
-    const size_t item = ((size_t)(b * a.n_head + head) * ((a.S + 63) / 64) + qt);
-    const __amdgpu_buffer_rsrc_t rp = attn_rsrc(a.pf_ws + item * nspl * 64 * rs);
+    const size_t item = ((size_t)(b * a.n_head + head) * ((a.S + QB - 1) / QB) + qt);
+    const __amdgpu_buffer_rsrc_t rp = attn_rsrc(a.pf_ws + item * nspl * QB * rs);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const int ql = w * 16 + 4 * g + i;
-      const uint32_t rec = (uint32_t)((spl * 64 + ql) * rs) * 4;
+      const uint32_t rec = (uint32_t)((spl * QB + ql) * rs) * 4;
       if (r == 0) {
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m_run[i]), rp, rec, 0, 16);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l_run[i]), rp, rec + 4, 0, 16);
@@ -2744,7 +2759,7 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       f32x4 og[G][NC];
 #pragma unroll
       for (int u = 0; u < G; u++) {
-        const uint32_t rec = (uint32_t)((min(s0 + u, nspl - 1) * 64 + ql) * rs) * 4;
+        const uint32_t rec = (uint32_t)((min(s0 + u, nspl - 1) * QB + ql) * rs) * 4;
         mg[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, rec, 0, 16));
         lg[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, rec + 4, 0, 16));
 #pragma unroll
@@ -2770,7 +2785,7 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnArgs a) {
       }
       M = mn;
     }
-    const int q = qt * 64 + ql;
+    const int q = qt * QB + ql;
     if (q < a.S) {
       const float inv = 1.f / Lsum;
       bf16* op = (bf16*)a.ctx_out + ((size_t)b * a.S + q) * a.hidden + head * hd;
@@ -2823,6 +2838,26 @@ int attention_decode_splits(int B, int n_head, int max_chunks) {
   return max(1, min(nsplit, 64));
 }
 
+// split-KV: a query tile's keys over ceil(tiles / pf_tiles) blocks when the grid would leave CUs idle and the
+// partials fit (the longest query tile otherwise walks every key tile alone).  QW waves per block (QW x 16 queries).
+template <int QW>
+static void attn_prefill_mfma_launch(const AttnArgs& a, hipStream_t s) {
+  constexpr int QB = QW * 16;
+  const int nqt = (a.S + QB - 1) / QB;
+  const int ktiles = (a.pf_past_max + a.S + 63) / 64;  // the last query tile's, longest row
+  int nspl = 1;
+  if (a.pf_tiles > 0 && a.pf_ws && a.pf_tickets && (long)nqt * a.n_head * a.B < 256 * 4 / QW && ktiles > a.pf_tiles) {
+    nspl = (ktiles + a.pf_tiles - 1) / a.pf_tiles;
+    const size_t need = (size_t)a.B * a.n_head * nqt * nspl * QB * (a.head_dim + 4);
+    if (need > a.pf_cap || (long)a.B * a.n_head * nqt > a.pf_ntickets) nspl = 1;
+  }
+  dim3 g(nqt * nspl, a.n_head, a.B);
+  const int hdp = (a.head_dim + 31) / 32 * 32;
+  if (hdp <= 64) attn_prefill_mfma_kernel<64, true, QW><<<g, QW * 64, 0, s>>>(a);
+  else if (hdp <= 96) attn_prefill_mfma_kernel<96, true, QW><<<g, QW * 64, 0, s>>>(a);
+  else attn_prefill_mfma_kernel<128, true, QW><<<g, QW * 64, 0, s>>>(a);
+}
+
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
   if (a.S == 1) {
     // Split partials merge either in the consumer (defer_merge, attn_merge.h) or, by ticket, in
@@ -2848,19 +2883,7 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
     if (is_bf16 && a.head_dim <= 128) {
       // split-KV: a query tile's keys over ceil(tiles / pf_tiles) blocks when the grid would leave CUs idle
       // and the partials fit (the longest query tile otherwise walks every key tile alone)
-      const int nqt = (a.S + 63) / 64;
-      const int ktiles = (a.pf_past_max + a.S + 63) / 64;  // the last query tile's, longest row
-      int nspl = 1;
-      if (a.pf_tiles > 0 && a.pf_ws && a.pf_tickets && (long)nqt * a.n_head * a.B < 256 && ktiles > a.pf_tiles) {
-        nspl = (ktiles + a.pf_tiles - 1) / a.pf_tiles;
-        const size_t need = (size_t)a.B * a.n_head * nqt * nspl * 64 * (a.head_dim + 4);
-        if (need > a.pf_cap || (long)a.B * a.n_head * nqt > a.pf_ntickets) nspl = 1;
-      }
-      dim3 g(nqt * nspl, a.n_head, a.B);
-      const int hdp = (a.head_dim + 31) / 32 * 32;
-      if (hdp <= 64) attn_prefill_mfma_kernel<64><<<g, 256, 0, s>>>(a);
-      else if (hdp <= 96) attn_prefill_mfma_kernel<96><<<g, 256, 0, s>>>(a);
-      else attn_prefill_mfma_kernel<128><<<g, 256, 0, s>>>(a);
+      attn_prefill_mfma_launch<4>(a, s);
     } else {
       dim3 g(a.S, a.n_head, a.B);
       if (is_bf16) attn_prefill_kernel<bf16><<<g, 64, 0, s>>>(a);

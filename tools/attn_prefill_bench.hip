@@ -64,6 +64,22 @@ int main() {
       printf("%-18s B=%d S=%4d past=%4d nh=%2d hd=%3d  pf_tiles=%d  median %7.2f us  min %7.2f  max|diff| %.3g\n", sh.name,
              sh.B, sh.S, sh.past, sh.nh, sh.hd, pt, t[t.size() / 2], t[0], md);
     }
+    // 32-query blocks (2 waves): twice the blocks, each staging a key tile for half the queries
+    for (int pt : {0, 2, 4}) {
+      a.pf_tiles = pt;
+      std::vector<float> t;
+      for (int it = 0; it < 25; it++) {
+        CK(hipEventRecord(e0)); attn_prefill_mfma_launch<2>(a, 0); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        if (it >= 5) t.push_back(ms * 1e3f);
+      }
+      std::sort(t.begin(), t.end());
+      CK(hipMemcpy(ho.data(), ctx, on * 2, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (size_t i = 0; i < on; i++) md = std::max(md, (double)fabsf((float)ho[i] - (float)hr[i]));
+      printf("%-18s B=%d S=%4d past=%4d nh=%2d hd=%3d  QW=2 pf_tiles=%d  median %7.2f us  min %7.2f  max|diff| %.3g\n",
+             sh.name, sh.B, sh.S, sh.past, sh.nh, sh.hd, pt, t[t.size() / 2], t[0], md);
+    }
   }
   return 0;
 }
