@@ -26,7 +26,10 @@ int main() {
       {"7b1 fc1", 512, 16384, 4096}, {"7b1 fc2", 512, 4096, 16384}, {"3b dense B2", 1024, 2560, 2560},
       // long prompts / batched prefill: >= 512 tiles (the 2-stage, two-blocks-per-CU question)
       {"7b1 qkv 2k", 2048, 12288, 4096}, {"7b1 fc1 1k", 1024, 16384, 4096}, {"7b1 dense 2k", 2048, 4096, 4096},
-      {"1b1 fc1 4k", 4096, 6144, 1536}, {"1b1 qkv 4k", 4096, 4608, 1536}};
+      {"1b1 fc1 4k", 4096, 6144, 1536}, {"1b1 qkv 4k", 4096, 4608, 1536},
+      // bloom-1b1 at 1024 / 2048 tokens (288..1536 tiles: where whole-tile grids of 384 / 512 blocks might apply)
+      {"1b1 qkv 1k", 1024, 4608, 1536}, {"1b1 fc1 1k", 1024, 6144, 1536}, {"1b1 fc2 1k", 1024, 1536, 6144},
+      {"1b1 qkv 2k", 2048, 4608, 1536}, {"1b1 fc1 2k", 2048, 6144, 1536}, {"1b1 fc2 2k", 2048, 1536, 6144}};
   bf16 *X, *W, *bias; float *out, *ref, *resid, *ws; unsigned* tick;
   const size_t MMAX = 4096;
   CK(hipMalloc(&X, MMAX * 16384 * 2)); CK(hipMalloc(&W, (size_t)16384 * 16384 * 2));
