@@ -47,6 +47,12 @@ def parse(argv=None):
     p.add_argument("--no-strong", action="store_true", help="pipeline: skip the fixed-rows (strong) measurement")
     p.add_argument("--no-configs", action="store_true",
                    help="pipeline: skip the BASELINE.json configs[3] / configs[4] records")
+    p.add_argument("--no-replicas", action="store_true",
+                   help="pipeline: skip the replicas record (the whole model on every GPU, same total rows)")
+    p.add_argument("--configs2-model", default="bloom-3b", help="configs[2]: model (uneven split at N = 4)")
+    p.add_argument("--configs2-batch", default="1,8", help="configs[2]: batch sizes B")
+    p.add_argument("--configs2-prompt", type=int, default=64, help="configs[2]: prompt tokens per row")
+    p.add_argument("--configs2-steps", type=int, default=128, help="configs[2]: timed decode rounds")
     p.add_argument("--configs-model", default="bloom-7b1", help="pipeline: model of the configs[3] / [4] records")
     p.add_argument("--configs3-mb", type=int, default=8, help="configs[3]: micro-batches of one row (B)")
     p.add_argument("--configs3-prompt", type=int, default=512, help="configs[3]: prefill tokens per row")
@@ -423,11 +429,26 @@ def main(argv=None):
     else:
         res = bench_single(args)
         if not args.no_pipeline_n1:
-            p1, _, _ = _pipeline(args)
-            res["pipeline_n1"] = {k: p1[k] for k in ("value", "ms_per_step", "config", "weak_definition", "stage_hbm",
-                                                     "prefill", "strong", "configs3", "configs4") if k in p1}
-            res["pipeline_n1"]["note"] = ("pipeline_bench.bench_pipeline at N = 1 (nccl world-1 group, StageExecutor, "
-                                          "graph-replayed decode): the same code and definitions as the N > 1 lines")
+            # the N = 1 point of the pipeline curve and its configs records ride on the headline: a failure there
+            # (out of memory on a shared GPU, a 7b1-shape error) is reported in the line, never loses it
+            try:
+                p1, _, _ = _pipeline(args)
+                res["pipeline_n1"] = {k: p1[k] for k in ("value", "ms_per_step", "config", "weak_definition",
+                                                         "scaling_ref", "stage_hbm", "prefill", "strong", "configs2",
+                                                         "configs3", "configs4", "replicas") if k in p1}
+                res["pipeline_n1"]["note"] = ("pipeline_bench.bench_pipeline at N = 1 (nccl world-1 group, "
+                                              "StageExecutor, graph-replayed decode): the same code and definitions "
+                                              "as the N > 1 lines")
+            except Exception as e:  # noqa: BLE001 -- recorded in the line, the headline stands
+                import traceback
+                traceback.print_exc()
+                res["pipeline_n1"] = {"error": f"{type(e).__name__}: {e}"}
+                try:
+                    import torch.distributed as dist
+                    if dist.is_initialized():
+                        dist.destroy_process_group()
+                except Exception:  # noqa: BLE001
+                    pass
         from distributed_inference_demo_amd import config
         model = config.get(args.model)
     if res is not None and args.cpu_baseline:  # rank 0, after the process group is gone

@@ -1,0 +1,85 @@
+"""Does the host keep ahead of the GPU at 16 micro-batches per round?  (VERDICT r4 "next" #6)
+
+The N = 8 stage shape of bloom-1b1: 3 layers (24 / 8) per stage, 16 one-row micro-batches in flight
+(2N, the reference's core_pool_size, Communication.java:418-437), and a 1/8 slice of the tied lm_head
+(vocabulary-parallel head).  On one GPU that stage runs as a world-1 Pipeline (no RCCL on the data path):
+
+  host_us_per_mb : host wall time of one Pipeline.step(1) round / 16 (ctypes bs_forward + the pipeline's
+                   Python bookkeeping per micro-batch), with the stream kept busy by a spin so the host never
+                   waits on the GPU
+  gpu_us_per_mb  : GPU time of one round / 16 (HIP events around 20 rounds, replays back to back)
+  rccl_us        : host cost of one RCCL call on this box (a 1-element all_reduce on the world-1 nccl group,
+                   enqueue only); an N = 8 middle rank issues ~5 per micro-batch (irecv + wait, isend, and
+                   2 + 2 on the head ring), so host_us_per_mb + 5 * rccl_us models the N = 8 host cost.
+Prints one JSON line.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (before the library: torch's libamdhip64 must serve the process)
+import torch.distributed as dist  # noqa: E402
+
+from distributed_inference_demo_amd import config  # noqa: E402
+from distributed_inference_demo_amd.pipeline import build_rank, init_distributed  # noqa: E402
+from distributed_inference_demo_amd.stage import Stage  # noqa: E402
+
+
+def main():
+    os.environ.setdefault("MASTER_PORT", "29533")
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    init_distributed("nccl")
+    dev = torch.device("cuda", 0)
+    n_mb, P, rounds = int(os.environ.get("N_MB", "16")), 64, 20
+    m = config.BloomDims("bloom-1b1/8-stage", 1536, 3, 16, vocab=31360)  # 3 layers + a 1/8 head slice
+    pipe, _ = build_rank(m, 0, 1, dev, mb_rows=1, n_mb=n_mb, max_ctx=P + 4 * rounds + 8, max_seq=P, head_split=False)
+    cs = torch.cuda.Stream()
+    torch.cuda.set_stream(cs)
+    prompt = torch.randint(0, m.vocab, (n_mb, P), dtype=torch.int32, device=dev)
+    pipe.step(P, prompt=prompt)
+    for _ in range(3):
+        pipe.step(1)
+    torch.cuda.synchronize()
+    # GPU time per round: replays back to back, HIP events on the stage stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    Stage.stream_delay(cs.cuda_stream, 20000)
+    e0.record(cs)
+    for _ in range(rounds):
+        pipe.step(1)
+    e1.record(cs)
+    torch.cuda.synchronize()
+    gpu_ms = e0.elapsed_time(e1) / rounds
+    # host time per round, the stream busy with a spin the whole time (enqueue never blocks on the GPU)
+    Stage.stream_delay(cs.cuda_stream, 200000)
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        pipe.step(1)
+    host_ms = (time.perf_counter() - t0) * 1e3 / rounds
+    torch.cuda.synchronize()
+    # one RCCL call's host cost (enqueue only, stream busy)
+    x = torch.zeros(1, device=dev)
+    dist.all_reduce(x)
+    torch.cuda.synchronize()
+    Stage.stream_delay(cs.cuda_stream, 200000)
+    t0 = time.perf_counter()
+    for _ in range(200):
+        dist.all_reduce(x)
+    rccl_us = (time.perf_counter() - t0) * 1e6 / 200
+    torch.cuda.synchronize()
+    host_mb, gpu_mb = host_ms * 1e3 / n_mb, gpu_ms * 1e3 / n_mb
+    res = {"shape": f"bloom-1b1 N = 8 stage: 3 layers, {n_mb} one-row micro-batches, vocab slice {m.vocab}",
+           "host_us_per_mb": host_mb, "gpu_us_per_mb": gpu_mb, "host_over_gpu": host_mb / gpu_mb,
+           "rccl_call_host_us": rccl_us,
+           "modeled_n8_host_us_per_mb": host_mb + 5 * rccl_us,
+           "modeled_n8_host_over_gpu": (host_mb + 5 * rccl_us) / gpu_mb}
+    print(json.dumps(res))
+    pipe.ex.stage.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
