@@ -97,13 +97,24 @@ class Pipeline:
         self.past = [0] * n_mb
         self.tokens_held = False  # after finish(): rank 0 already holds every micro-batch's next input
         if self.head_split:
-            self.xn = [torch.empty(mb_rows * hidden, dtype=act_dtype, device=device) for _ in range(n_mb)]
-            self.kin = [torch.zeros(mb_rows, dtype=torch.int64, device=device) for _ in range(n_mb)]
-            self.kout = [torch.zeros(mb_rows, dtype=torch.int64, device=device) for _ in range(n_mb)]
+            # one packed ring message per micro-batch: [xn (mb x h, activation dtype) | argmax keys (mb x int64)],
+            # so a ring hop is ONE send and ONE receive (each RCCL call costs the host ~8-11 us: tools/host_enqueue.py);
+            # ring ranks fold their slice into the keys in place (bs_head_slice allows keys_in == keys_out).
+            # prefill_row's one-row passes use a one-row message of the same layout.
+            self.hmsg, self.xn, self.hkeys = self._ring_buffers(mb_rows, hidden, act_dtype, device, n_mb)
+            self.pmsg, self.pxn, self.pkeys = self._ring_buffers(1, hidden, act_dtype, device, n_mb)
             cuda = device.type == "cuda"
             self.hstream = torch.cuda.Stream(device) if cuda else None
             self.tok_ready = [torch.cuda.Event() for _ in range(n_mb)] if cuda else None
             self.closer = world - 2  # rank whose slice closes the head ring
+
+    @staticmethod
+    def _ring_buffers(rows, hidden, act_dtype, device, n):
+        esz = torch.tensor([], dtype=act_dtype).element_size()
+        nx = rows * hidden * esz
+        nx8 = (nx + 7) // 8 * 8
+        msgs = [torch.zeros(nx8 + 8 * rows, dtype=torch.uint8, device=device) for _ in range(n)]
+        return msgs, [m[:nx].view(act_dtype) for m in msgs], [m[nx8:].view(torch.int64) for m in msgs]
 
     @staticmethod
     def _drain(lst):
@@ -121,19 +132,17 @@ class Pipeline:
         with self._hctx():
             self._drain(self.hpending[j])
             self._drain(self.tsend[j])
-            _recv(self.xn[j], prev, self.head_group)
-            _recv(self.kin[j], prev, self.head_group)
+            _recv(self.hmsg[j], prev, self.head_group)
             if self.rank == self.closer:
-                self.ex.head_slice(self.xn[j], self.mb, self.kin[j], None, self.tok[j])
+                self.ex.head_slice(self.xn[j], self.mb, self.hkeys[j], None, self.tok[j])
                 if self.rank == 0:
                     if self.tok_ready is not None:
                         self.tok_ready[j].record()
                 else:
                     self.tsend[j].append(dist.isend(self.tok[j], dst=0, group=self.tok_group))
             else:
-                self.ex.head_slice(self.xn[j], self.mb, self.kin[j], self.kout[j], None)
-                self.hpending[j].append(dist.isend(self.xn[j], dst=self.rank + 1, group=self.head_group))
-                self.hpending[j].append(dist.isend(self.kout[j], dst=self.rank + 1, group=self.head_group))
+                self.ex.head_slice(self.xn[j], self.mb, self.hkeys[j], self.hkeys[j], None)
+                self.hpending[j].append(dist.isend(self.hmsg[j], dst=self.rank + 1, group=self.head_group))
 
     def _token_in(self, j, record):
         """Rank 0: the token of micro-batch j from the previous round."""
@@ -206,9 +215,8 @@ class Pipeline:
                     self.pending[j].append(dist.isend(out, dst=self.rank + 1))
                 else:  # head_split: open the head ring with ln_f and this rank's slice
                     self.ex.head_norm(out, self.mb, seq, self.xn[j])
-                    self.ex.head_slice(self.xn[j], self.mb, None, self.kout[j], None)
-                    self.pending[j].append(dist.isend(self.xn[j], dst=0, group=self.head_group))
-                    self.pending[j].append(dist.isend(self.kout[j], dst=0, group=self.head_group))
+                    self.ex.head_slice(self.xn[j], self.mb, None, self.hkeys[j], None)
+                    self.pending[j].append(dist.isend(self.hmsg[j], dst=0, group=self.head_group))
             if self.head_split and self.rank <= self.closer:
                 self._head_role(j, record)
             self.past[j] = [p + seq for p in self.past[j]] if isinstance(self.past[j], list) else self.past[j] + seq
@@ -220,7 +228,7 @@ class Pipeline:
         `ids` int32 [1, n] on rank 0 (None elsewhere).  The first generated token lands in self.pf_tok[j][r] on
         rank 0 (stream-ordered); it travels on `pf_group`, so it never interleaves with the decode rounds'
         token returns on `tok_group`.  Every rank calls this in the same order as every other rank."""
-        n_el, h = n * self.h, self.h
+        n_el = n * self.h
         slot = j * self.mb + r
         tok = self.pf_tok[j][r:r + 1]
         self._drain(self.pending[j])
@@ -239,24 +247,21 @@ class Pipeline:
             if not self.is_last:
                 self.pending[j].append(dist.isend(out, dst=self.rank + 1))
             else:  # head_split: open the head ring
-                self.ex.head_norm(out, 1, n, self.xn[j][:h])
-                self.ex.head_slice(self.xn[j][:h], 1, None, self.kout[j][:1], None)
-                self.pending[j].append(dist.isend(self.xn[j][:h], dst=0, group=self.head_group))
-                self.pending[j].append(dist.isend(self.kout[j][:1], dst=0, group=self.head_group))
+                self.ex.head_norm(out, 1, n, self.pxn[j])
+                self.ex.head_slice(self.pxn[j], 1, None, self.pkeys[j], None)
+                self.pending[j].append(dist.isend(self.pmsg[j], dst=0, group=self.head_group))
         if self.head_split and self.rank <= self.closer:
             prev = self.world - 1 if self.rank == 0 else self.rank - 1
             with self._hctx():
                 self._drain(self.hpending[j])
-                _recv(self.xn[j][:h], prev, self.head_group)
-                _recv(self.kin[j][:1], prev, self.head_group)
+                _recv(self.pmsg[j], prev, self.head_group)
                 if self.rank == self.closer:
-                    self.ex.head_slice(self.xn[j][:h], 1, self.kin[j][:1], None, tok)
+                    self.ex.head_slice(self.pxn[j], 1, self.pkeys[j], None, tok)
                     if self.rank != 0:
                         self.hpending[j].append(dist.isend(tok, dst=0, group=self.pf_group))
                 else:
-                    self.ex.head_slice(self.xn[j][:h], 1, self.kin[j][:1], self.kout[j][:1], None)
-                    self.hpending[j].append(dist.isend(self.xn[j][:h], dst=self.rank + 1, group=self.head_group))
-                    self.hpending[j].append(dist.isend(self.kout[j][:1], dst=self.rank + 1, group=self.head_group))
+                    self.ex.head_slice(self.pxn[j], 1, self.pkeys[j], self.pkeys[j], None)
+                    self.hpending[j].append(dist.isend(self.pmsg[j], dst=self.rank + 1, group=self.head_group))
             if self.rank == 0 and self.closer == 0 and self.hstream is not None:
                 torch.cuda.current_stream().wait_stream(self.hstream)
         if self.is_first and self.world > 1 and not (self.head_split and self.closer == 0):

@@ -150,7 +150,8 @@ int bs_forward(bs_stage *stage, const bs_step *step, const void *in, void *out, 
 int bs_head_norm(bs_stage *stage, const float *hidden, int32_t batch, int32_t seq, void *xn, void *stream);
 /* Logits of the stage's vocabulary slice for xn [B][hidden]; writes per-row keys
  * max(keys_in[b], slice max) to keys_out (either may be NULL) and, when tokens is non-NULL,
- * the decoded token ids.  Device pointers, stream ordered. */
+ * the decoded token ids.  keys_out may equal keys_in (the merge is per row, in place).  Device pointers,
+ * stream ordered. */
 int bs_head_slice(bs_stage *stage, const void *xn, int32_t batch, const uint64_t *keys_in, uint64_t *keys_out,
                   int32_t *tokens, void *stream);
 

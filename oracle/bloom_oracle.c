@@ -183,19 +183,61 @@ void or_destroy(or_stage *s) {
 }
 
 static inline float rb(const or_stage *s, float v) { return s->bf16 ? gen_bf16_round(v) : v; }
+/* v rounded to the nearest fp16 value (ties to even), as a float: 11 significant bits, subnormals below
+ * 2^-14 in steps of 2^-24, |v| >= 65520 -> inf (what the device's float -> _Float16 conversion does) */
+static inline float rf16(float v) {
+  const float a = fabsf(v);
+  if (a != a) return v;
+  if (a >= 65520.f) return copysignf(INFINITY, v);
+  float q;
+  if (a < 6.103515625e-05f) {
+    q = 5.9604644775390625e-08f;
+  } else {
+    int e;
+    frexpf(a, &e);
+    q = ldexpf(1.f, e - 11);
+  }
+  return copysignf(rintf(a / q) * q, v);
+}
+void or_round_fp16(const float *in, float *out, uint64_t n) { for (uint64_t i = 0; i < n; i++) out[i] = rf16(in[i]); }
 
-static int g_accum_double = 0; /* test knob: accumulate dot products in double */
-void or_set_accum_double(int on) { g_accum_double = on; }
+/* test knob: dot-product accumulation order.  0: 16 fp32 lanes + a tree (default), 1: double,
+ * 2: one sequential fp32 accumulator, 3: fp32 sums of 32-element chunks added in order (the K-step
+ * grouping of the device's MFMA GEMMs).  Modes 0, 2 and 3 are three correct fp32 orders of the same
+ * rounded math; their spread against mode 1 is the format's own noise (tools/parity_study.py). */
+static int g_accum_mode = 0;
+void or_set_accum_double(int on) { g_accum_mode = on ? 1 : 0; }
+void or_set_accum_mode(int mode) { g_accum_mode = mode; }
+/* test knob (bit mask) for the P.V product of the attention, emulating device roundings the bf16 mode does
+ * not model: 1 = V rounded to fp16 (|V| > 65504 -> inf), 2 = P = fp16(p) + fp16(p - fp16(p)), 4 = P =
+ * bf16(p) + bf16(p - bf16(p)); with any bit set P is exp(s - max) unnormalised and the context is divided
+ * by the sum after the product (the device's order).  0: the HF order (normalised p, fp32). */
+static int g_emul_pv = 0;
+void or_set_emul_pv(int mask) { g_emul_pv = mask; }
 /* diagnostic knob: bits of bf16 rounding points to SKIP (1 LN out, 2 K/V, 4 q, 8 ctx, 16 GELU out) */
 static int g_skip_round = 0;
 void or_set_skip_round(int mask) { g_skip_round = mask; }
 static inline float rbp(const or_stage *s, int point, float v) { return (g_skip_round & point) ? v : rb(s, v); }
 
 static float dotf(const float *a, const float *b, int K) {
-  if (g_accum_double) {
+  if (g_accum_mode == 1) {
     double d = 0.0;
     for (int k = 0; k < K; k++) d += (double)a[k] * (double)b[k];
     return (float)d;
+  }
+  if (g_accum_mode == 2) {
+    float t = 0.f;
+    for (int k = 0; k < K; k++) t += a[k] * b[k];
+    return t;
+  }
+  if (g_accum_mode == 3) {
+    float t = 0.f;
+    for (int k0 = 0; k0 < K; k0 += 32) {
+      float c = 0.f;
+      for (int k = k0; k < K && k < k0 + 32; k++) c += a[k] * b[k];
+      t += c;
+    }
+    return t;
   }
   float acc[16] = {0};
   int k = 0;
@@ -310,10 +352,24 @@ int or_forward(or_stage *s, int B, int S, int slot, int past_len, const void *in
           float inv = 1.0f / sum;
           float *o = ctx + (size_t)m * h + (size_t)hh * hd;
           for (int d = 0; d < hd; d++) o[d] = 0.f;
-          for (int j = 0; j < nk; j++) {
-            const float *vr = kv_ptr(s, li, 1, slot + b, hh, j);
-            float p = sc[j] * inv;
-            for (int d = 0; d < hd; d++) o[d] += p * vr[d];
+          if (g_emul_pv) {
+            for (int j = 0; j < nk; j++) {
+              const float *vr = kv_ptr(s, li, 1, slot + b, hh, j);
+              float e = sc[j], hi = e, lo = 0.f;
+              if (g_emul_pv & 2) { hi = rf16(e); lo = rf16(e - hi); }
+              else if (g_emul_pv & 4) { hi = gen_bf16_round(e); lo = gen_bf16_round(e - hi); }
+              for (int d = 0; d < hd; d++) {
+                float v = (g_emul_pv & 1) ? rf16(vr[d]) : vr[d];
+                o[d] += hi * v + lo * v;
+              }
+            }
+            for (int d = 0; d < hd; d++) o[d] *= inv;
+          } else {
+            for (int j = 0; j < nk; j++) {
+              const float *vr = kv_ptr(s, li, 1, slot + b, hh, j);
+              float p = sc[j] * inv;
+              for (int d = 0; d < hd; d++) o[d] += p * vr[d];
+            }
           }
           for (int d = 0; d < hd; d++) o[d] = rbp(s, 8, o[d]);
         }

@@ -30,6 +30,9 @@ def lib():
         L.or_write_kv.restype = ctypes.c_int
         L.or_write_kv.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 4 + [ctypes.c_void_p]
         L.or_set_accum_double.argtypes = [ctypes.c_int]
+        L.or_set_accum_mode.argtypes = [ctypes.c_int]
+        L.or_set_emul_pv.argtypes = [ctypes.c_int]
+        L.or_round_fp16.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
         L.or_set_skip_round.argtypes = [ctypes.c_int]
         L.or_quantize_int8.restype = ctypes.c_int
         L.or_quantize_int8.argtypes = [ctypes.c_void_p]
@@ -60,6 +63,32 @@ def alibi_slopes(n_head):
     out = np.empty(n_head, dtype=np.float32)
     lib().or_alibi_slopes(n_head, _p(out))
     return out
+
+
+def round_fp16(x):
+    """The checker's fp32 -> fp16 rounding (or_set_emul_pv bit 1), for its test against numpy."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    lib().or_round_fp16(_p(x), _p(out), x.size)
+    return out
+
+
+class checker_mode:
+    """Context manager: the checker's accumulation order (or_set_accum_mode) and P.V emulation
+    (or_set_emul_pv) for the calls inside the block -- global knobs of liboracle."""
+
+    def __init__(self, accum=0, emul_pv=0):
+        self.accum, self.emul = accum, emul_pv
+
+    def __enter__(self):
+        lib().or_set_accum_mode(self.accum)
+        lib().or_set_emul_pv(self.emul)
+        return self
+
+    def __exit__(self, *a):
+        lib().or_set_accum_mode(0)
+        lib().or_set_emul_pv(0)
+        return False
 
 
 def num_threads():

@@ -54,7 +54,7 @@ def main():
     torch.cuda.synchronize()
     gpu_ms = e0.elapsed_time(e1) / rounds
     # host time per round, the stream busy with a spin the whole time (enqueue never blocks on the GPU)
-    Stage.stream_delay(cs.cuda_stream, 200000)
+    Stage.stream_delay(cs.cuda_stream, 100000)
     t0 = time.perf_counter()
     for _ in range(rounds):
         pipe.step(1)
@@ -64,7 +64,7 @@ def main():
     x = torch.zeros(1, device=dev)
     dist.all_reduce(x)
     torch.cuda.synchronize()
-    Stage.stream_delay(cs.cuda_stream, 200000)
+    Stage.stream_delay(cs.cuda_stream, 100000)
     t0 = time.perf_counter()
     for _ in range(200):
         dist.all_reduce(x)
