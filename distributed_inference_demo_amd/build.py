@@ -17,7 +17,9 @@ LIB = os.path.join(PKG, "lib", "libbloomstage.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "stage.hip", "codec.cpp", "safetensors.cpp"]
+SOURCES = ["kernels.hip", "attn_prefill.hip", "stage.hip", "codec.cpp", "safetensors.cpp"]
+# per-source extra flags: the prefill attention keeps its MFMA accumulators in VGPRs (attn_prefill.hip header)
+EXTRA = {"attn_prefill.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 HEADERS = ["common.h", "kernels.h", "attn_merge.h", "safetensors.h"]
 STAMP = os.path.join(OBJ, "build_id")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
@@ -57,6 +59,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
                 flags = [f for f in flags if not f.startswith("--offload-arch")] + ["-x", "c++"]
             if src == "stage.hip":
                 flags.append(f'-DBS_BUILD_ID="{bid}"')
+            flags += EXTRA.get(src, [])
             jobs.append([HIPCC] + flags + ["-c", sp, "-o", op])
 
     def run(cmd):

@@ -11,9 +11,9 @@ gemv_ldsw4<T = 4>, (4096, 16384) split-K) and decode attention at B * heads = 51
 The checker (oracle/bloom_oracle.c, bf16 mode) cannot afford 2000 decode steps of 32 rows at this width,
 so between checkpoints the device runs free (its own argmax tokens) and at each checkpoint the device
 cache written since the last one is handed to the checker (bs_read_kv -> or_write_kv); then both run the
-checkpoint step from the same token: ids equal unless the checker's top-2 margin is < 2e-2, logits within
-north_star's 2e-2 plus the checker's own measured noise (its fp32 vs float64 accumulations, ~2e-2 at this
-width) of the float64-accumulating checker, mean-abs <= 4e-3 (check_logits_wide), and the K/V rows the step
+checkpoint step from the same token: ids equal unless the checker's top-2 margin is < 2e-2, logits within the
+constant bounds of check_logits_wide (max-abs 3e-2, mean-abs 4.5e-3 from the float64-accumulating checker, fixed from
+the multi-seed study profiles/r05_parity_study.txt), and the K/V rows the step
 appends (the device's QKV epilogue vs the checker's projection) within the wide-block hidden-state bound plus
 one bf16 storage ulp (check_bf16_stored: cached values are rounded to bf16, and two correct paths may round a
 value in [4, 8) to neighbours 0.03125 apart).  The prompt's cache is the checker's own and is
@@ -32,26 +32,30 @@ from oracle import gen_np
 from oracle.oracle import OracleStage
 
 from oracle.oracle import lib as oracle_lib
-from test_gpu_parity import BF16_TOL, assert_ids_match, check_bf16_stored, check_close, record_error
+from test_gpu_parity import assert_ids_match, check_bf16_stored, check_close, record_error
 
-WIDE_LOGIT_MEAN_TOL = 4e-3
+# Logits at h = 4096 against the float64-accumulating checker: constants stated before the run, from the committed
+# multi-seed study (tools/parity_study.py -> profiles/r05_parity_study.txt): over 8 seeds, 2 layers, V = 4096, B = 16
+# (and B = 32), every CORRECT fp32 evaluation of the same bf16-rounded math -- the checker's three summation orders,
+# with and without the device's P.V roundings emulated -- lands 0.0165-0.0243 max-abs / <= 0.0037 mean-abs from the
+# float64 one, and the device inside that spread (0.0198-0.0240 / <= 0.0039).  One bf16 rounding flip of an
+# intermediate, which two correct fp32 orders disagree on, moves a logit ~1e-2 at this width; the max over 65k-131k
+# logits of that noise is ~2e-2 by itself.  The bounds sit one noise quantum above the study's worst correct order.
+WIDE_LOGIT_MAX_TOL = 3.0e-2
+WIDE_LOGIT_MEAN_TOL = 4.5e-3
 
 
 def check_logits_wide(got, ref32, ref64, what):
-    """Logits at h = 4096, against the checker with float64 dot-product accumulation (or_set_accum_double; the
-    same bf16 storage points): max-abs <= north_star's 2e-2 + d_ref, mean-abs <= 4e-3, where d_ref is the
-    distance between the checker's own two accumulations (fp32 and float64) on the same inputs, measured in
-    this call.  At this width d_ref is itself ~2e-2 (profiles/r04_parity_errors.json: 0.0203-0.0211 max-abs,
-    3.4e-3 mean at the prefill, max |logit| ~25): one bf16 rounding flip of an intermediate, which two correct
-    fp32 summation orders of the same math disagree on, moves a logit that far, so a flat 2e-2 sits at the
-    format's noise floor and the device -- a third correct order -- gets the tolerance on top of it.  Every
-    distance is recorded (gpurun_out/parity_errors.jsonl)."""
-    d_ref = record_error(f"{what} [fp32 checker vs float64 checker]", ref32, ref64, 0.0, "checker noise")
-    record_error(f"{what} [device vs fp32 checker]", got, ref32, BF16_TOL + d_ref, "logits bf16 (recorded)")
-    bound = BF16_TOL + d_ref
-    err = record_error(what, got, ref64, bound, "logits bf16 vs float64 checker")
+    """Logits at h = 4096 against the checker with float64 dot-product accumulation (or_set_accum_double; the same bf16
+    storage points): max-abs <= WIDE_LOGIT_MAX_TOL and mean-abs <= WIDE_LOGIT_MEAN_TOL, constants (above).  The fp32
+    checker's own distance to the float64 one and the device's distance to the fp32 checker are recorded beside it
+    ($BS_PARITY_LOG), not asserted."""
+    record_error(f"{what} [fp32 checker vs float64 checker]", ref32, ref64, 0.0, "checker noise")
+    record_error(f"{what} [device vs fp32 checker]", got, ref32, WIDE_LOGIT_MAX_TOL, "logits bf16 (recorded)")
+    err = record_error(what, got, ref64, WIDE_LOGIT_MAX_TOL, "logits bf16 vs float64 checker")
     mean = float(np.abs(got - ref64).mean())
-    assert err <= bound and mean <= WIDE_LOGIT_MEAN_TOL, f"{what}: logits max-abs {err} (bound {bound}), mean-abs {mean}"
+    assert err <= WIDE_LOGIT_MAX_TOL and mean <= WIDE_LOGIT_MEAN_TOL, \
+        f"{what}: logits max-abs {err} (bound {WIDE_LOGIT_MAX_TOL}), mean-abs {mean} (bound {WIDE_LOGIT_MEAN_TOL})"
     return err
 
 

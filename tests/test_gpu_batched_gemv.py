@@ -74,3 +74,24 @@ def test_batched_decode_middle_stage_offset_rows(B):
         check_close(yg, yo, "bf16", f"B={B} offset-rows decode step {step}")
     gs.close()
     os_.close()
+
+
+@pytest.mark.parametrize("h,nh", [(1024, 16), (2560, 32), (4096, 32)])
+@pytest.mark.parametrize("B", [5, 7, 8])
+def test_small_batch_decode_middle_stage_widths(h, nh, B):
+    """4 < B <= 8 at the 560m / 3b / 7b1 widths (ln_rows_wave_kernel + gemv_ldsw4, split-K on the N = h GEMVs): a
+    2-layer middle stage fed offset rows at a slot offset decodes 3 steps within the wide-block bound."""
+    from test_gpu_parity import check_close
+    L, V = 3, 1024
+    gs, os_ = pair(h, nh, L, V, 1, 3, "bf16", seed=41, max_batch=B + 1, max_ctx=16, max_tokens=B * 4, is_first=False,
+                   is_last=False)
+    rng = np.random.default_rng(9)
+    x = (5.0 + rng.standard_normal((B, 4, h))).astype(np.float32)
+    check_close(gs.forward_host(x, B, 4, slot=1, past_len=0), os_.forward(x, B, 4, slot=1, past_len=0), "bf16",
+                f"h={h} B={B} prefill")
+    for step in range(3):
+        x1 = (5.0 + rng.standard_normal((B, 1, h))).astype(np.float32)
+        check_close(gs.forward_host(x1, B, 1, slot=1, past_len=4 + step), os_.forward(x1, B, 1, slot=1, past_len=4 + step),
+                    "bf16", f"h={h} B={B} decode step {step}")
+    gs.close()
+    os_.close()

@@ -163,3 +163,62 @@ def test_7b1_batch32_two_stage_decode_to_ctx_516_bf16_equals_one_stage():
         for (layer, row), kv in res[r][3].items():
             assert np.array_equal(kv, one.read_kv(layer, row, P - 4, STEPS + 4)), (r, layer, row)
     one.close()
+
+
+SERVE_M = config.BloomDims("serve-small", 256, 4, 4, vocab=1024)
+
+
+def _serve_worker(rank, world, port, q, kw):
+    from distributed_inference_demo_amd.serve import RunConfig, run_rank
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      OMP_NUM_THREADS="2")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = {}
+        for prefill in (True, False):
+            cfg = RunConfig(model=SERVE_M, num_sample=5, max_length=6, core_pool_size=2, prompt_len=7, dtype="fp32",
+                            seed=kw["seed"], head_split=True, prefill=prefill)
+
+            def factory(lb, le, first, last, max_batch, max_ctx, hslice):
+                return HipHostExecutor(SERVE_M, "fp32", kw["seed"], lb, le, first, last, max_batch, max_ctx, 16, hslice)
+            res = run_rank(cfg, rank, world, torch.device("cpu"), executor_factory=factory)
+            out[prefill] = None if res is None else res["samples"]
+            dist.barrier()
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_serve_head_split_ring_on_product_stages(world):
+    """serve.run_rank with the vocabulary-parallel head ring (head_split) at world 2 and 3, the PRODUCT stages on cuda:0
+    as gloo ranks: the admission prefill passes (Pipeline.prefill_row: one pass per admitted sample, its first token back
+    from the ring's closer on its own communicator) give the same samples as the token-a-round feed (prefill=False), and
+    both equal the fp32 checker decoding each sample alone.  (The ring's hstream / RCCL branches run only on an RCCL
+    group: the driver's multi-GPU run.)"""
+    from distributed_inference_demo_amd.serve import RunConfig, synthetic_prompts
+    from oracle.oracle import OracleStage
+    seed = 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_serve_worker, args=(r, world, port, q, {"seed": seed})) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[True] == out[False]
+    cfg = RunConfig(model=SERVE_M, num_sample=5, max_length=6, core_pool_size=2, prompt_len=7, dtype="fp32", seed=seed)
+    for sid, p in enumerate(synthetic_prompts(cfg, SERVE_M.vocab)):
+        st = OracleStage(SERVE_M.hidden, SERVE_M.n_head, SERVE_M.n_layer, SERVE_M.vocab, 0, SERVE_M.n_layer, max_batch=1,
+                         max_ctx=len(p) + 8, seed=seed)
+        tok = st.forward(np.array(p, np.int32).reshape(1, -1), 1, len(p))
+        ids = [int(tok[0])]
+        for i in range(5):
+            tok = st.forward(tok.reshape(1, 1), 1, 1, past_len=len(p) + i)
+            ids.append(int(tok[0]))
+        assert out[True][sid] == ids, (sid, out[True][sid], ids)

@@ -37,8 +37,15 @@ VARIANTS = {"f64": (1, 0), "fp32_lanes": (0, 0), "fp32_seq": (2, 0), "fp32_k32":
             "emul_fp16": (0, 1 | 2), "emul_bf16": (0, 4)}
 
 
+BATCH = {}  # --batch override: rows per L (file tag L{L}B{B})
+
+
 def shape(L):
-    return (16, P) if L == 2 else (8, P)
+    return (BATCH.get(L) or (16 if L == 2 else 8), P)
+
+
+def tag(L):
+    return f"L{L}" if L not in BATCH else f"L{L}B{BATCH[L]}"
 
 
 def inputs(seed, L):
@@ -53,7 +60,7 @@ def run_cpu(layers, seeds):
     for L in layers:
         B, S = shape(L)
         for seed in seeds:
-            out = os.path.join(CPU_DIR, f"ref_L{L}_s{seed}.npz")
+            out = os.path.join(CPU_DIR, f"ref_{tag(L)}_s{seed}.npz")
             if os.path.exists(out):
                 continue
             ids, nxt = inputs(seed, L)
@@ -69,7 +76,7 @@ def run_cpu(layers, seeds):
             np.savez(out, **res)
 
 
-def run_gpu(layers, seeds, tag):
+def run_gpu(layers, seeds, dtag):
     import torch  # noqa: F401  (torch's HIP runtime first)
     from distributed_inference_demo_amd.stage import Stage
     os.makedirs(GPU_DIR, exist_ok=True)
@@ -81,15 +88,16 @@ def run_gpu(layers, seeds, tag):
             _, pre = g.forward_host(ids, B, S, past_len=0, want_logits=True)
             _, dec = g.forward_host(nxt, B, 1, past_len=S, want_logits=True)
             g.close()
-            np.savez(os.path.join(GPU_DIR, f"dev_{tag}_L{L}_s{seed}.npz"), prefill=pre, decode=dec)
-            print(f"device {tag} L={L} seed={seed}", flush=True)
+            np.savez(os.path.join(GPU_DIR, f"dev_{dtag}_{tag(L)}_s{seed}.npz"), prefill=pre, decode=dec)
+            print(f"device {dtag} {tag(L)} seed={seed}", flush=True)
 
 
 def report(out_prefix):
     rows = []
     for f in sorted(glob.glob(os.path.join(CPU_DIR, "ref_L*_s*.npz"))):
-        base = os.path.basename(f)[4:-4]  # L{L}_s{seed}
-        L, seed = int(base.split("_")[0][1:]), int(base.split("_")[1][1:])
+        base = os.path.basename(f)[4:-4]  # L{L}[B{B}]_s{seed}
+        lt, seed = base.split("_")[0][1:], int(base.split("_")[1][1:])
+        L, B = (int(lt.split("B")[0]), int(lt.split("B")[1])) if "B" in lt else (int(lt), 16 if lt == "2" else 8)
         ref = np.load(f)
         cands = {k[:-len("_prefill")]: None for k in ref.files if k.endswith("_prefill") and not k.startswith("f64")}
         for dev in sorted(glob.glob(os.path.join(GPU_DIR, f"dev_*_{base}.npz"))):
@@ -98,7 +106,7 @@ def report(out_prefix):
             for ph in ("prefill", "decode"):
                 got = ref[f"{name}_{ph}"] if dv is None else dv[ph]
                 d = np.abs(got.astype(np.float64) - ref[f"f64_{ph}"])
-                rows.append({"L": L, "seed": seed, "phase": ph, "variant": name, "max_abs": float(d.max()),
+                rows.append({"L": L, "B": B, "seed": seed, "phase": ph, "variant": name, "max_abs": float(d.max()),
                              "mean_abs": float(d.mean()), "max_ref": float(np.abs(ref[f"f64_{ph}"]).max()),
                              "n": int(d.size)})
     with open(out_prefix + ".jsonl", "w") as f:
@@ -106,12 +114,12 @@ def report(out_prefix):
             f.write(json.dumps(r) + "\n")
     lines = ["distance to the float64-accumulating checker (same bf16 storage points), logits of the last position",
              "per (L, phase, variant): max-abs over seeds [min .. max] and mean over seeds; mean-abs max over seeds", ""]
-    keys = sorted({(r["L"], r["phase"], r["variant"]) for r in rows})
-    for L, ph, var in keys:
-        sel = [r for r in rows if (r["L"], r["phase"], r["variant"]) == (L, ph, var)]
+    keys = sorted({(r["L"], r["B"], r["phase"], r["variant"]) for r in rows})
+    for L, B, ph, var in keys:
+        sel = [r for r in rows if (r["L"], r["B"], r["phase"], r["variant"]) == (L, B, ph, var)]
         mx = [r["max_abs"] for r in sel]
         mn = [r["mean_abs"] for r in sel]
-        lines.append(f"L={L:2d} {ph:7s} {var:22s} seeds={len(sel)} max-abs [{min(mx):.4f} .. {max(mx):.4f}] "
+        lines.append(f"L={L:2d} B={B:2d} {ph:7s} {var:22s} seeds={len(sel)} max-abs [{min(mx):.4f} .. {max(mx):.4f}] "
                      f"mean {np.mean(mx):.4f}   mean-abs max {max(mn):.5f}")
     open(out_prefix + ".txt", "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
@@ -123,9 +131,12 @@ def main():
     ap.add_argument("--layers", default="2,30")
     ap.add_argument("--seeds", type=int, default=8)
     ap.add_argument("--tag", default="lib")
+    ap.add_argument("--batch", type=int, default=0, help="rows (default 16 at L = 2, 8 at L = 30)")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r05_parity_study"))
     a = ap.parse_args()
     layers = [int(x) for x in a.layers.split(",")]
+    if a.batch:
+        BATCH.update({L: a.batch for L in layers})
     seeds = list(range(101, 101 + a.seeds))
     if a.phase == "cpu":
         run_cpu(layers, seeds)
