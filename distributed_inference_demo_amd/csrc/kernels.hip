@@ -750,16 +750,20 @@ __device__ __forceinline__ void emb_rows_finish(const LnArgs& ln, int M, int K, 
 // 2 = no activation loads (x = 1), 4 = no epilogue (a store that never fires keeps the math).
 // Block = blockDim.x / 64 waves (1..16): the dispatch sizes blocks so the grid is ~one block per CU
 // and every CU streams the same number of weight bytes (gemv_rows_dispatch).
-template <int R, int MM, int U, int XM, int FL = 0, int LB = 256>  // LB: threads the registers are bounded for
-__global__ __launch_bounds__(LB) void gemv_rows_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
-                                                         LnArgs ln, AttnParts pa, int M, int N, int K, Epi ep) {
+// The block body, shared with attn_dense_kernel: block `bid`.  wait != nullptr (X_PARTS in attn_dense_kernel): the
+// split-attention partials come from the SAME launch -- the weight stream is issued first, then one lane polls *wait
+// (sc1 loads) until it reaches `target` (bounded: ~0.2 s, then wait[2] = 1 records the timeout), the block meets
+// at a barrier, and every partial load is an sc1 load (MI355X_MICROARCH.md "Valid forms" row 1).
+template <int R, int MM, int U, int XM, int FL = 0>
+__device__ __forceinline__ void gemv_rows_block(const bf16* __restrict__ W, const bf16* __restrict__ X, const LnArgs& ln,
+                                                const AttnParts& pa, int M, int N, int K, const Epi& ep, int bid,
+                                                char* smem, unsigned* wait, unsigned target) {
   constexpr bool LN = XM == X_LN;
   BS_STAMP(0);
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   float* scratch = reinterpret_cast<float*>(smem);                  // 64 floats
   bf16* xs = reinterpret_cast<bf16*>(smem + 256);                    // LN / PARTS: [M][K]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int n0 = (blockIdx.x * nw + w) * R;
+  const int n0 = (bid * nw + w) * R;
   const bf16* wr[R];
 #pragma unroll
   for (int r = 0; r < R; r++) wr[r] = W + (size_t)min(n0 + r, N - 1) * K;
@@ -780,13 +784,23 @@ __global__ __launch_bounds__(LB) void gemv_rows_kernel(const bf16* __restrict__ 
   if constexpr (XM == X_EMB) emb_rows_prefetch<MM>(ln, M, K, eid, egb, gb);
   const int kq = K >> 2, ngroups = M * kq;  // PARTS: 4-column groups of all rows
   PartsRegs pr[XM == X_PARTS ? kPartsPre : 1];
-  auto pld1 = [](const float* p, size_t i) { return p[i]; };
-  auto pld4 = [](const float* p, size_t i) { return *reinterpret_cast<const float4*>(p + i); };
+  // plain loads after a kernel boundary; sc1 loads (L2-coherent across XCDs) for partials of the same launch
+  auto pld1 = [wait](const float* p, size_t i) {
+    if (wait) return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(attn_rsrc(p), (uint32_t)(i * 4), 0, 16));
+    return p[i];
+  };
+  auto pld4 = [wait](const float* p, size_t i) {
+    if (wait)
+      return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(attn_rsrc(p), (uint32_t)(i * 4), 0, 16));
+    return *reinterpret_cast<const float4*>(p + i);
+  };
   if constexpr (XM == X_PARTS) {
+    if (!wait) {
 #pragma unroll
-    for (int it = 0; it < kPartsPre; it++) {
-      const int g = min((int)threadIdx.x + it * (int)blockDim.x, ngroups - 1);
-      attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, pr[it]);
+      for (int it = 0; it < kPartsPre; it++) {
+        const int g = min((int)threadIdx.x + it * (int)blockDim.x, ngroups - 1);
+        attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, pr[it]);
+      }
     }
   }
   bf16x8 wv[U][R];
@@ -805,6 +819,24 @@ __global__ __launch_bounds__(LB) void gemv_rows_kernel(const bf16* __restrict__ 
     emb_rows_finish<MM>(ln, M, K, eid, egb, gb, xs, scratch);
     xg = xs; xstride = K;
   } else if constexpr (XM == X_PARTS) {
+    if (wait) {  // the attention blocks of this launch: poll, then every partial load below is sc1
+      if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while (__builtin_amdgcn_raw_buffer_load_b32(attn_rsrc(wait), 0, 0, 16) < target) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1u << 22)) {
+            __builtin_amdgcn_raw_buffer_store_b32(1u, attn_rsrc(wait), 8, 0, 16);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < kPartsPre; it++) {
+        const int g = min((int)threadIdx.x + it * (int)blockDim.x, ngroups - 1);
+        attn_parts_load(pa, g / kq, (g % kq) * 4, pld1, pld4, pr[it]);
+      }
+    }
     auto put = [&](int g, const PartsRegs& r) {
       float o[4];
       attn_parts_combine(pa.nsplit, r, o);
@@ -903,6 +935,13 @@ __global__ __launch_bounds__(LB) void gemv_rows_kernel(const bf16* __restrict__ 
     }
   });
   BS_STAMP(3);
+}
+
+template <int R, int MM, int U, int XM, int FL = 0, int LB = 256>  // LB: threads the registers are bounded for
+__global__ __launch_bounds__(LB) void gemv_rows_kernel(const bf16* __restrict__ W, const bf16* __restrict__ X,
+                                                         LnArgs ln, AttnParts pa, int M, int N, int K, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  gemv_rows_block<R, MM, U, XM, FL>(W, X, ln, pa, M, N, K, ep, blockIdx.x, smem, nullptr, 0u);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2262,8 +2301,12 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
 // ticket of its (row, head) merges all partials (sc1 loads, issued together) and writes ctx —
 // MI355X_MICROARCH.md "Valid forms" row 1 (counter form, the last adder reads).
 
-template <typename T, int WV, int CH = 64>  // CH: positions per wave chunk (64 or 32)
-__global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
+// The block body, shared with attn_dense_kernel: block (head, b, sp) of nsplit.  `done` (attn_dense_kernel): the
+// partials go out write-through (sc1) and, after every wave's stores drained, one lane adds 1 to *done (agent
+// scope) -- MI355X_MICROARCH.md "Valid forms" row 1 (ONE lane of each storing workgroup, sc1 payload both sides).
+template <typename T, int WV, int CH>
+__device__ __forceinline__ void attn_decode_block(const AttnArgs& a, int head, int b, int sp, int nsplit,
+                                                  unsigned* done) {
   constexpr int NI = CH / 4;  // load instructions per chunk (4 rows each)
   __shared__ __attribute__((aligned(16))) float qs[128];
   __shared__ float es[WV][64];
@@ -2271,7 +2314,6 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   __shared__ float pacc[WV][128];
   __shared__ int last;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int head = blockIdx.x, b = blockIdx.y, sp = blockIdx.z, nsplit = gridDim.z;
   const int hd = a.head_dim;
   const size_t rowbase = ((size_t)(a.slot + b) * a.n_head + head) * a.max_ctx;
   const T* kb = (const T*)a.k_cache + rowbase * hd;
@@ -2388,6 +2430,21 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
   const size_t pair = (size_t)(a.slot + b) * a.n_head + head;
   float* pacc_g = a.part_acc + pair * a.max_chunks * hd;  // [nsplit][hd]
   float* pml_g = a.part_ml + pair * a.max_chunks * 2;     // [nsplit][2]
+  if (done) {  // attn_dense_kernel: the same launch's dense blocks merge (attn_merge.h), sc1 both sides
+    if (threadIdx.x < hd)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), attn_rsrc(pacc_g), (uint32_t)(sp * hd + threadIdx.x) * 4, 0, 16);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(M), attn_rsrc(pml_g), (uint32_t)sp * 8, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(L), attn_rsrc(pml_g), (uint32_t)sp * 8 + 4, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      typedef __attribute__((address_space(1))) unsigned gu32;
+      __hip_atomic_fetch_add((gu32*)done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   if (a.defer_merge) {  // the consumer merges (attn_merge.h): plain stores, the kernel boundary publishes
     if (threadIdx.x < hd) pacc_g[sp * hd + threadIdx.x] = o;
     if (threadIdx.x == 0) { pml_g[sp * 2] = M; pml_g[sp * 2 + 1] = L; }
@@ -2446,6 +2503,11 @@ __global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
     }
     ctx[threadIdx.x] = from_f32<T>(acc2 / lsum);
   }
+}
+
+template <typename T, int WV, int CH = 64>  // CH: positions per wave chunk (64 or 32)
+__global__ __launch_bounds__(WV * 64) void attn_decode_kernel(AttnArgs a) {
+  attn_decode_block<T, WV, CH>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z, nullptr);
 }
 
 // S > 1: one wave per (query, head, row), online softmax over 64-key blocks.
@@ -2551,6 +2613,73 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
       if (is_bf16) attn_prefill_kernel<bf16><<<g, 64, 0, s>>>(a);
       else attn_prefill_kernel<float><<<g, 64, 0, s>>>(a);
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Split decode attention + the dense GEMV in ONE launch (B <= 2, bf16).  Blocks [0, n_attn) are the
+// attention's (head, row, split) blocks (attn_decode_block, 8 waves x 32 positions); each publishes its
+// partial sc1 and adds 1 to sync[0].  Blocks [n_attn, n_attn + n_dense) are 8-wave rows-GEMV blocks
+// (gemv_rows_block, X_PARTS): they issue their first U weight chunks, one lane polls sync[0] up to n_attn,
+// the block merges the partials (sc1 loads) into LDS and streams the rest of the rows.  The dense weights
+// are in flight while the attention runs, and the kernel boundary between the two is gone.  The last
+// dense block (ticket on sync[1]) resets both words for the next launch.  Only for grids of <= 256 blocks:
+// one block per CU keeps every block resident, so no poller waits on an undispatched producer; every
+// spin is bounded anyway (sync[2] = 1 records a timeout).
+template <int MM, int U>
+__global__ __launch_bounds__(512) void attn_dense_kernel(AttnArgs a, AttnParts pa, const bf16* __restrict__ W, int M,
+                                                         int N, int K, Epi ep, int nsplit, int n_attn, int n_dense,
+                                                         unsigned* sync) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bid = blockIdx.x;
+  if (bid < n_attn) {
+    const int head = bid % a.n_head, rest = bid / a.n_head;
+    attn_decode_block<bf16, 8, 32>(a, head, rest % a.B, rest / a.B, nsplit, sync);
+    return;
+  }
+  gemv_rows_block<1, MM, U, X_PARTS>(W, nullptr, LnArgs{}, pa, M, N, K, ep, bid - n_attn, smem, sync,
+                                     (unsigned)n_attn);
+  if (threadIdx.x == 0) {  // this lane's poll matched above: the last dense block resets the words
+    typedef __attribute__((address_space(1))) unsigned gu32;
+    const unsigned old = __hip_atomic_fetch_add((gu32*)(sync + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned)n_dense - 1) {
+      __hip_atomic_store((gu32*)sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32*)(sync + 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+bool attn_dense_supported(int M, int N, int K, int n_head, int head_dim, int nsplit) {
+  const int n_attn = M * n_head * nsplit, n_dense = (N + 7) / 8;
+  return M >= 1 && M <= 2 && nsplit >= 2 && nsplit <= kPartsMaxSplit && head_dim <= 128 && head_dim % 8 == 0 &&
+         K % 512 == 0 && K <= 4096 && K == n_head * head_dim && n_attn + n_dense <= 256;
+}
+
+void launch_attn_dense(const AttnArgs& a, const void* W, int M, int N, int K, const Epi& ep, unsigned* sync,
+                       hipStream_t s) {
+  const int nsplit = attention_decode_splits(a.B, a.n_head, a.max_chunks);
+  const AttnParts pa{a.part_acc, a.part_ml, nsplit, a.n_head, a.head_dim, a.max_chunks, a.slot};
+  const int n_attn = M * a.n_head * nsplit, n_dense = (N + 7) / 8;
+  const size_t shm = 256 + (size_t)M * K * sizeof(bf16);
+  // U: 512-column chunks per row in flight, the rows_plan choice for 8-wave R = 1 blocks (<= 8 registers' worth)
+  const int cpr = K / 512;
+  const int u = cpr <= 3 || cpr == 5 || cpr == 8 ? cpr : (cpr % 4 == 0 ? 4 : (cpr % 2 == 0 ? 2 : 1));
+  auto go = [&](auto mc, auto uc) {
+    constexpr int MMc = decltype(mc)::value, Uc = decltype(uc)::value;
+    attn_dense_kernel<MMc, Uc><<<n_attn + n_dense, 512, shm, s>>>(a, pa, (const bf16*)W, M, N, K, ep, nsplit,
+                                                                  n_attn, n_dense, sync);
+  };
+  auto gm = [&](auto uc) {
+    if (M == 1) go(EpiKindC<1>{}, uc);
+    else go(EpiKindC<2>{}, uc);
+  };
+  switch (u) {
+    case 1: gm(EpiKindC<1>{}); break;
+    case 2: gm(EpiKindC<2>{}); break;
+    case 3: gm(EpiKindC<3>{}); break;
+    case 5: gm(EpiKindC<5>{}); break;
+    case 8: gm(EpiKindC<8>{}); break;
+    default: gm(EpiKindC<4>{}); break;
   }
 }
 

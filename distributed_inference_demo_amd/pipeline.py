@@ -28,14 +28,20 @@ from .placement import stage_ranges
 
 
 class StageExecutor:
-    """Product executor: a libbloomstage Stage fed device tensors on the current stream."""
+    """Product executor: a libbloomstage Stage fed device tensors on the current stream.  Pipeline.step hands it the
+    round's stream handle once (set_stream) so the per-micro-batch forward does not look it up through torch again
+    (tools/host_enqueue.py: the host enqueue per micro-batch is what an N = 8 rank must keep ahead of the GPU)."""
 
     def __init__(self, stage):
         self.stage = stage
+        self._sh = None
+
+    def set_stream(self, handle):
+        self._sh = handle
 
     def forward(self, inp, out, batch, seq, slot, past_len):
-        self.stage.forward(inp, out, batch, seq, slot=slot, past_len=past_len,
-                           stream=torch.cuda.current_stream().cuda_stream)
+        sh = self._sh if self._sh is not None else torch.cuda.current_stream().cuda_stream
+        self.stage.forward(inp, out, batch, seq, slot=slot, past_len=past_len, stream=sh)
 
     def head_norm(self, hidden, batch, seq, xn):
         self.stage.head_norm(hidden, batch, seq, xn, stream=torch.cuda.current_stream().cuda_stream)
@@ -96,6 +102,7 @@ class Pipeline:
         self.tsend = [[] for _ in range(n_mb)]
         self.past = [0] * n_mb
         self.tokens_held = False  # after finish(): rank 0 already holds every micro-batch's next input
+        self._views = {}  # (buffer list id, micro-batch, elements) -> the sliced view (a torch slice costs ~3 us)
         if self.head_split:
             # one packed ring message per micro-batch: [xn (mb x h, activation dtype) | argmax keys (mb x int64)],
             # so a ring hop is ONE send and ONE receive (each RCCL call costs the host ~8-11 us: tools/host_enqueue.py);
@@ -107,6 +114,13 @@ class Pipeline:
             self.hstream = torch.cuda.Stream(device) if cuda else None
             self.tok_ready = [torch.cuda.Event() for _ in range(n_mb)] if cuda else None
             self.closer = world - 2  # rank whose slice closes the head ring
+
+    def _view(self, bufs, j, n):
+        key = (id(bufs), j, n)
+        v = self._views.get(key)
+        if v is None:
+            v = self._views[key] = bufs[j][:n]
+        return v
 
     @staticmethod
     def _ring_buffers(rows, hidden, act_dtype, device, n):
@@ -183,6 +197,8 @@ class Pipeline:
         forward of this round is appended -- HIP events on CUDA ranks, host-clock ms otherwise (stage
         busy time, pipeline_bench's prefill overlap)."""
         n_el = self.mb * seq * self.h
+        if self.dev.type == "cuda" and hasattr(self.ex, "set_stream"):
+            self.ex.set_stream(torch.cuda.current_stream().cuda_stream)
         for j in range(self.n_mb):
             slot = j * self.mb
             if pasts is not None:
@@ -200,7 +216,7 @@ class Pipeline:
                     if feed is not None:
                         inp = torch.where(feed[j][1], feed[j][0], inp)
             else:
-                inp = self.hin[j][:n_el]
+                inp = self._view(self.hin, j, n_el)
                 _recv(inp, self.rank - 1)
             if self.is_last and not self.head_split:
                 self._forward(inp, self.tok[j], seq, slot, j, timing)
@@ -209,7 +225,7 @@ class Pipeline:
                 elif record is not None:
                     record[j].append(self.tok[j].clone())
             else:
-                out = self.hout[j][:n_el]
+                out = self._view(self.hout, j, n_el)
                 self._forward(inp, out, seq, slot, j, timing)
                 if not self.is_last:
                     self.pending[j].append(dist.isend(out, dst=self.rank + 1))

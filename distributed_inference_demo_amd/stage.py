@@ -209,6 +209,8 @@ class Stage:
             _check(lib().bs_init_stage(ctypes.byref(d), ctypes.byref(h)))
         self._h = h
         self._weights_ref = None  # uploaded; host copy no longer needed
+        self._steps = {}  # decode fast path: re-used Step structs
+        self._fwd = lib().bs_forward
         self.past = [0] * max_batch  # host mirror of cached positions per KV row
 
     def _step(self, batch, seq, slot, past_len, flags):
@@ -216,6 +218,13 @@ class Stage:
         Returns (step, per-row pasts)."""
         if past_len is None:
             past_len = self.past[slot:slot + batch] if 0 <= slot and slot + batch <= len(self.past) else 0
+        if isinstance(past_len, int):  # the decode fast path: a Step per (batch, seq, slot, flags), re-used
+            key = (batch, seq, slot, flags)
+            st = self._steps.get(key)
+            if st is None:
+                st = self._steps[key] = Step(batch, seq, slot, past_len, flags, None)
+            st.past_len = past_len
+            return st, None
         if np.ndim(past_len) == 0:
             pasts = [int(past_len)] * batch
             st = Step(batch, seq, slot, int(past_len), flags, None)
@@ -233,9 +242,12 @@ class Stage:
         """past_len: positions already cached, one int for every row or one per row (None: the
         host mirror of each row's position)."""
         st, pasts = self._step(batch, seq, slot, past_len, BS_STEP_LOGITS if logits is not None else 0)
-        _check(lib().bs_forward(self._h, ctypes.byref(st), _ptr(inp), _ptr(out), _ptr(logits), stream))
-        for i, r in enumerate(range(slot, slot + batch)):
-            self.past[r] = pasts[i] + seq
+        _check(self._fwd(self._h, ctypes.byref(st), _ptr(inp), _ptr(out), _ptr(logits), stream))
+        if pasts is None:
+            self.past[slot:slot + batch] = [st.past_len + seq] * batch
+        else:
+            for i, r in enumerate(range(slot, slot + batch)):
+                self.past[r] = pasts[i] + seq
         return out
 
     def set_sampling(self, top_k=1, temperature=1.0, seed=0):
@@ -268,8 +280,11 @@ class Stage:
         st, pasts = self._step(batch, seq, slot, past_len, flags)
         _check(lib().bs_forward(self._h, ctypes.byref(st), x.ctypes.data, out.ctypes.data,
                                 logits.ctypes.data if logits is not None else None, None))
-        for i, r in enumerate(range(slot, slot + batch)):
-            self.past[r] = pasts[i] + seq
+        if pasts is None:
+            self.past[slot:slot + batch] = [st.past_len + seq] * batch
+        else:
+            for i, r in enumerate(range(slot, slot + batch)):
+                self.past[r] = pasts[i] + seq
         return (out, logits) if want_logits else out
 
     def reset(self, slot=-1):

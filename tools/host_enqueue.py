@@ -9,8 +9,9 @@ The N = 8 stage shape of bloom-1b1: 3 layers (24 / 8) per stage, 16 one-row micr
                    waits on the GPU
   gpu_us_per_mb  : GPU time of one round / 16 (HIP events around 20 rounds, replays back to back)
   rccl_us        : host cost of one RCCL call on this box (a 1-element all_reduce on the world-1 nccl group,
-                   enqueue only); an N = 8 middle rank issues ~5 per micro-batch (irecv + wait, isend, and
-                   2 + 2 on the head ring), so host_us_per_mb + 5 * rccl_us models the N = 8 host cost.
+                   enqueue only); an N = 8 middle rank issues 4 per micro-batch (irecv + wait, isend, and one
+                   packed receive + one packed send on the head ring), so host_us_per_mb + 4 * rccl_us models
+                   the N = 8 host cost.
 Prints one JSON line.
 """
 import json
@@ -70,12 +71,39 @@ def main():
         dist.all_reduce(x)
     rccl_us = (time.perf_counter() - t0) * 1e6 / 200
     torch.cuda.synchronize()
+    # the pieces of one micro-batch's enqueue (stream busy): torch's current-stream handle, one Stage.forward
+    # (Step struct + ctypes + bs_forward's graph launch), and a bare bs_forward with a prebuilt Step
+    import ctypes
+    from distributed_inference_demo_amd.stage import Step, lib
+    Stage.stream_delay(cs.cuda_stream, 100000)
+    t0 = time.perf_counter()
+    for _ in range(1000):
+        torch.cuda.current_stream().cuda_stream
+    cur_us = (time.perf_counter() - t0) * 1e3
+    st = pipe.ex.stage
+    tok = pipe.tok[0]
+    past = st.past[0]
+    t0 = time.perf_counter()
+    for _ in range(200):
+        st.forward(tok, tok, 1, 1, slot=0, past_len=past, stream=cs.cuda_stream)
+    fwd_us = (time.perf_counter() - t0) * 1e6 / 200
+    torch.cuda.synchronize()
+    Stage.stream_delay(cs.cuda_stream, 100000)
+    stp = Step(1, 1, 0, past, 0, None)
+    L, h, ip, sh = lib(), st._h, tok.data_ptr(), cs.cuda_stream
+    t0 = time.perf_counter()
+    for _ in range(200):
+        L.bs_forward(h, ctypes.byref(stp), ip, ip, None, sh)
+    raw_us = (time.perf_counter() - t0) * 1e6 / 200
+    torch.cuda.synchronize()
     host_mb, gpu_mb = host_ms * 1e3 / n_mb, gpu_ms * 1e3 / n_mb
     res = {"shape": f"bloom-1b1 N = 8 stage: 3 layers, {n_mb} one-row micro-batches, vocab slice {m.vocab}",
            "host_us_per_mb": host_mb, "gpu_us_per_mb": gpu_mb, "host_over_gpu": host_mb / gpu_mb,
-           "rccl_call_host_us": rccl_us,
-           "modeled_n8_host_us_per_mb": host_mb + 5 * rccl_us,
-           "modeled_n8_host_over_gpu": (host_mb + 5 * rccl_us) / gpu_mb}
+           "rccl_call_host_us": rccl_us, "current_stream_handle_us": cur_us, "stage_forward_us": fwd_us,
+           "bare_bs_forward_us": raw_us,
+           "n8_middle_rank_rccl_calls_per_mb": 4,
+           "modeled_n8_host_us_per_mb": host_mb + 4 * rccl_us,
+           "modeled_n8_host_over_gpu": (host_mb + 4 * rccl_us) / gpu_mb}
     print(json.dumps(res))
     pipe.ex.stage.close()
     dist.destroy_process_group()
