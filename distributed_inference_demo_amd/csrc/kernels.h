@@ -117,11 +117,6 @@ struct AttnParts {
 bool linear_parts_supported(int M, int K, int head_dim, int nsplit);
 // Weight GEMV on ctx = merge(partials) (bf16): the dense projection after a deferred-merge attention.
 void launch_linear_parts(const AttnParts& p, const void* W, int M, int N, int K, const Epi& ep, hipStream_t s);
-// Split decode attention and the dense GEMV (+ its epilogue) in one launch (kernels.hip attn_dense_kernel);
-// sync: 3 zeroed words the launch leaves zeroed.  Needs attn_dense_supported.
-bool attn_dense_supported(int M, int N, int K, int n_head, int head_dim, int nsplit);
-void launch_attn_dense(const AttnArgs& a, const void* W, int M, int N, int K, const Epi& ep, unsigned* sync,
-                       hipStream_t s);
 
 // keys -> token ids
 // Reduce the per-tile keys of each row (and keys_in[m] if given) -> keys_out[m] / tokens[m] (either optional).

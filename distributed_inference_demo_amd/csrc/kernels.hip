@@ -1162,9 +1162,14 @@ __device__ __forceinline__ bf16x8 q8x8_to_bf16(const uint2 raw) {
 // is 8 bytes converted in registers, the row scale applied by the epilogue's col_scale).
 // PD: stages in flight per wave (register ring): 2, or 3 when a wave's K part is exactly 3 stages (the
 // bloom-1b1 widths), so every load of the wave is issued before its first stage waits.
-template <int T, int WAVES, int MT, typename WT = bf16, int PD = 2>
+// LNS > 0 (bf16 weights, MT = 1, one K split): X is LN(ln.x) -- the LayerNorm runs in the prologue.  A wave's K
+// part is exactly LNS stages; its lanes load their fp32 activations of every stage (row r, the columns of their
+// B fragments) behind the first weight stages, take the shifted sums of ln_rows_wave_kernel over them, and the
+// 8 waves' sums meet in LDS (one barrier) -- the waves together cover the whole row.  The normalised bf16
+// fragments stay in registers for the whole K loop (no activation loads in it).
+template <int T, int WAVES, int MT, typename WT = bf16, int PD = 2, int LNS = 0>
 __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __restrict__ W, const bf16* __restrict__ X,
-                                                               int M, int N, int K, Epi ep) {
+                                                               int M, int N, int K, Epi ep, LnArgs ln) {
   constexpr int RB = 128, KC = RB / (int)sizeof(WT);  // bytes / columns of one row per stage
   constexpr int CPR = RB / 16, RPI = 64 / CPR, ROWS = T * 16, NI = ROWS / RPI, KSTEP = KC / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1224,7 +1229,91 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
       }
     __builtin_amdgcn_wave_barrier();
   };
-  if (nst > 0) {
+  if constexpr (LNS > 0) {
+    static_assert(MT == 1 && sizeof(WT) == 2, "LN prologue: one m-tile, bf16 weights");
+    auto loadw = [&](int st, u32x4v (&ww)[NI]) {
+      const size_t o = (size_t)st * KC;
+#pragma unroll
+      for (int i = 0; i < NI; i++) {
+        const WT* src = (RPI * i + lr < rows_ok) ? wsrc + i * wstep : wsrc;
+        ww[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(src + o));
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < PD - 1; p++)
+      if (p < LNS) loadw(p, wr[p]);
+    // row min(r, M - 1), columns kbeg + KC * st + 32 j + 8 g .. + 8: this lane's B fragments
+    const float* xrow = ln.x + ((size_t)min(r, M - 1) * ln.row_stride + ln.row_offset) * K;
+    float4 xf[LNS][KSTEP][2];
+    u32x4v gr[LNS][KSTEP], br[LNS][KSTEP];
+#pragma unroll
+    for (int st = 0; st < LNS; st++)
+#pragma unroll
+      for (int j = 0; j < KSTEP; j++) {
+        const int col = kbeg + st * KC + 32 * j + 8 * g;
+        xf[st][j][0] = *reinterpret_cast<const float4*>(xrow + col);
+        xf[st][j][1] = *reinterpret_cast<const float4*>(xrow + col + 4);
+        gr[st][j] = *reinterpret_cast<const u32x4v*>(ln.gamma + col);
+        br[st][j] = *reinterpret_cast<const u32x4v*>(ln.beta + col);
+      }
+    const float c = xrow[0];
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int st = 0; st < LNS; st++)
+#pragma unroll
+      for (int j = 0; j < KSTEP; j++)
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const float d0 = xf[st][j][h].x - c, d1 = xf[st][j][h].y - c, d2 = xf[st][j][h].z - c, d3 = xf[st][j][h].w - c;
+          a1 += (d0 + d1) + (d2 + d3);
+          a2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+        }
+    a1 += __shfl_xor(a1, 16, 64); a1 += __shfl_xor(a1, 32, 64);
+    a2 += __shfl_xor(a2, 16, 64); a2 += __shfl_xor(a2, 32, 64);
+    float* sred = red + WAVES * (T * 16) * (MT * 16 + 1);  // [WAVES][16][2], after the epilogue's area
+    if (g == 0) { sred[(w * 16 + r) * 2] = a1; sred[(w * 16 + r) * 2 + 1] = a2; }
+    __syncthreads();
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ww++) { t1 += sred[(ww * 16 + r) * 2]; t2 += sred[(ww * 16 + r) * 2 + 1]; }
+    const float invk = 1.0f / (float)K;
+    t1 *= invk; t2 *= invk;
+    const float mean = c + t1, rstd = 1.0f / sqrtf(fmaxf(t2 - t1 * t1, 0.f) + ln.eps);
+    bf16x8 xn[LNS][KSTEP];
+#pragma unroll
+    for (int st = 0; st < LNS; st++)
+#pragma unroll
+      for (int j = 0; j < KSTEP; j++) {
+        float4 g0, g1, b0, b1;
+        bf16x4_to_f32(make_uint2(gr[st][j].x, gr[st][j].y), g0);
+        bf16x4_to_f32(make_uint2(gr[st][j].z, gr[st][j].w), g1);
+        bf16x4_to_f32(make_uint2(br[st][j].x, br[st][j].y), b0);
+        bf16x4_to_f32(make_uint2(br[st][j].z, br[st][j].w), b1);
+        const float4 v0 = xf[st][j][0], v1 = xf[st][j][1];
+        bf16x8 o;
+        o[0] = (bf16)((v0.x - mean) * rstd * g0.x + b0.x); o[1] = (bf16)((v0.y - mean) * rstd * g0.y + b0.y);
+        o[2] = (bf16)((v0.z - mean) * rstd * g0.z + b0.z); o[3] = (bf16)((v0.w - mean) * rstd * g0.w + b0.w);
+        o[4] = (bf16)((v1.x - mean) * rstd * g1.x + b1.x); o[5] = (bf16)((v1.y - mean) * rstd * g1.y + b1.y);
+        o[6] = (bf16)((v1.z - mean) * rstd * g1.z + b1.z); o[7] = (bf16)((v1.w - mean) * rstd * g1.w + b1.w);
+        xn[st][j] = o;
+      }
+#pragma unroll
+    for (int st = 0; st < LNS; st++) {
+      const int b = st % PD;
+      if (st + PD - 1 < LNS) loadw(st + PD - 1, wr[(st + PD - 1) % PD]);
+#pragma unroll
+      for (int i = 0; i < NI; i++) *reinterpret_cast<u32x4v*>(&wl[swz(RPI * i + lr, lc * 16)]) = wr[b][i];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < KSTEP; j++)
+#pragma unroll
+        for (int t = 0; t < T; t++) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(&wl[swz(t * 16 + r, 64 * j + 16 * g)]);
+          acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, xn[st][j], acc[t][0], 0, 0, 0);
+        }
+      __builtin_amdgcn_wave_barrier();
+    }
+  } else if (nst > 0) {
 #pragma unroll
     for (int p = 0; p < PD - 1; p++)
       if (p < nst) load(p, wr[p], xr[p]);
@@ -1244,11 +1333,32 @@ static void gemv_ldsw4_launch(const bf16* X, const WT* W, int M, int N, int K, i
   constexpr int KC = 128 / (int)sizeof(WT);
   if constexpr (sizeof(WT) == 2) {
     if (K / (KS * WAVES * KC) == 3) {
-      gemv_ldsw4_kernel<T, WAVES, MT, WT, 3><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+      gemv_ldsw4_kernel<T, WAVES, MT, WT, 3><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep, LnArgs{});
       return;
     }
   }
-  gemv_ldsw4_kernel<T, WAVES, MT, WT, 2><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep);
+  gemv_ldsw4_kernel<T, WAVES, MT, WT, 2><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep, LnArgs{});
+}
+
+// LN-fused gemv_ldsw4 (bf16, M <= 16, one K split): a wave's K part is K / (8 * 64) stages, 2..5 supported.
+template <int T>
+static bool gemv_ldsw4_ln_launch(const LnArgs& ln, const bf16* W, int M, int N, int K, const Epi& ep, hipStream_t s) {
+  constexpr int WAVES = 8;
+  const int nst = K / (WAVES * 64);
+  if (M > 16 || K % (WAVES * 64) || nst < 2 || nst > 5) return false;
+  const size_t shm = (size_t)WAVES * T * 16 * 128 + sizeof(float) * WAVES * (T * 16) * 17 + sizeof(float) * WAVES * 32;
+  const int blocks = (N + T * 16 - 1) / (T * 16);
+  auto go = [&](auto pc, auto lc) {
+    constexpr int PDc = decltype(pc)::value, LNSc = decltype(lc)::value;
+    gemv_ldsw4_kernel<T, WAVES, 1, bf16, PDc, LNSc><<<blocks, WAVES * 64, shm, s>>>(W, nullptr, M, N, K, ep, ln);
+  };
+  switch (nst) {
+    case 2: go(EpiKindC<2>{}, EpiKindC<2>{}); break;
+    case 3: go(EpiKindC<3>{}, EpiKindC<3>{}); break;
+    case 4: go(EpiKindC<2>{}, EpiKindC<4>{}); break;
+    default: go(EpiKindC<3>{}, EpiKindC<5>{}); break;
+  }
+  return true;
 }
 
 template <int T, int MT, int WAVES, typename WT = bf16>
@@ -1279,8 +1389,11 @@ static const TileCfg kTileTable[] = {
   {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 2, 2, 8, 2, 2, 8},
 };
 
+// ln != nullptr (bf16): X = LN(ln->x) fused into gemv_ldsw4's prologue when the shape takes one K split of
+// 2..5 stages per wave and M <= 16; otherwise returns false and the caller normalises first.
 template <typename WT = bf16>
-static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K, const Epi& ep, hipStream_t s) {
+static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K, const Epi& ep, hipStream_t s,
+                                const LnArgs* ln = nullptr) {
   if (M <= 4 || M > 32 || (K % 64) != 0) return false;
   const int units = K / 64;
   int T = N >= 16384 ? 4 : 2, KS = 1, WV = 0;
@@ -1302,6 +1415,16 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
     // 36.4 -> 25.6, fc2 43.1 -> 32.0; decode steps: 7b1 B=16 +11 %, 3b B=8 +35 %, 1b1 B=8 +32 % over
     // gemv_tiles; profiles/r02_tiles_sweep.txt).  gemv_tiles takes the shapes whose K parts do not divide K.
     constexpr int KC = 128 / (int)sizeof(WT);
+    if (ln) {
+      if constexpr (sizeof(WT) == 2) {
+        if (KS != 1 || two || T > 4) return false;
+        if (T == 4) return gemv_ldsw4_ln_launch<4>(*ln, w, M, N, K, ep, s);
+        if (T == 3) return gemv_ldsw4_ln_launch<3>(*ln, w, M, N, K, ep, s);
+        if (T == 2) return gemv_ldsw4_ln_launch<2>(*ln, w, M, N, K, ep, s);
+        return gemv_ldsw4_ln_launch<1>(*ln, w, M, N, K, ep, s);
+      }
+      return false;
+    }
     if (T <= 4 && K % (KS * 8 * KC) == 0) {
       auto go4 = [&](auto tc) {
         constexpr int TT = decltype(tc)::value;
@@ -2197,6 +2320,10 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
     gemv_dispatch<true>(nullptr, ln, (const bf16*)W, M, N, K, ep, s);
     return;
   }
+  if (tiles && M <= 16) {  // LN in the batched GEMV's prologue (gemv_ldsw4 LNS)
+    const LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
+    if (gemv_tiles_dispatch<bf16>(nullptr, (const bf16*)W, M, N, K, ep, s, &ln)) return;
+  }
   if (is_bf16 && K <= 4096 && (K % 4) == 0) {
     LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
     launch_ln_rows_wave(ln, M, K, (bf16*)xn_scratch, s);
@@ -2613,73 +2740,6 @@ void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s) {
       if (is_bf16) attn_prefill_kernel<bf16><<<g, 64, 0, s>>>(a);
       else attn_prefill_kernel<float><<<g, 64, 0, s>>>(a);
     }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Split decode attention + the dense GEMV in ONE launch (B <= 2, bf16).  Blocks [0, n_attn) are the
-// attention's (head, row, split) blocks (attn_decode_block, 8 waves x 32 positions); each publishes its
-// partial sc1 and adds 1 to sync[0].  Blocks [n_attn, n_attn + n_dense) are 8-wave rows-GEMV blocks
-// (gemv_rows_block, X_PARTS): they issue their first U weight chunks, one lane polls sync[0] up to n_attn,
-// the block merges the partials (sc1 loads) into LDS and streams the rest of the rows.  The dense weights
-// are in flight while the attention runs, and the kernel boundary between the two is gone.  The last
-// dense block (ticket on sync[1]) resets both words for the next launch.  Only for grids of <= 256 blocks:
-// one block per CU keeps every block resident, so no poller waits on an undispatched producer; every
-// spin is bounded anyway (sync[2] = 1 records a timeout).
-template <int MM, int U>
-__global__ __launch_bounds__(512) void attn_dense_kernel(AttnArgs a, AttnParts pa, const bf16* __restrict__ W, int M,
-                                                         int N, int K, Epi ep, int nsplit, int n_attn, int n_dense,
-                                                         unsigned* sync) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int bid = blockIdx.x;
-  if (bid < n_attn) {
-    const int head = bid % a.n_head, rest = bid / a.n_head;
-    attn_decode_block<bf16, 8, 32>(a, head, rest % a.B, rest / a.B, nsplit, sync);
-    return;
-  }
-  gemv_rows_block<1, MM, U, X_PARTS>(W, nullptr, LnArgs{}, pa, M, N, K, ep, bid - n_attn, smem, sync,
-                                     (unsigned)n_attn);
-  if (threadIdx.x == 0) {  // this lane's poll matched above: the last dense block resets the words
-    typedef __attribute__((address_space(1))) unsigned gu32;
-    const unsigned old = __hip_atomic_fetch_add((gu32*)(sync + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == (unsigned)n_dense - 1) {
-      __hip_atomic_store((gu32*)sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gu32*)(sync + 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-bool attn_dense_supported(int M, int N, int K, int n_head, int head_dim, int nsplit) {
-  const int n_attn = M * n_head * nsplit, n_dense = (N + 7) / 8;
-  return M >= 1 && M <= 2 && nsplit >= 2 && nsplit <= kPartsMaxSplit && head_dim <= 128 && head_dim % 8 == 0 &&
-         K % 512 == 0 && K <= 4096 && K == n_head * head_dim && n_attn + n_dense <= 256;
-}
-
-void launch_attn_dense(const AttnArgs& a, const void* W, int M, int N, int K, const Epi& ep, unsigned* sync,
-                       hipStream_t s) {
-  const int nsplit = attention_decode_splits(a.B, a.n_head, a.max_chunks);
-  const AttnParts pa{a.part_acc, a.part_ml, nsplit, a.n_head, a.head_dim, a.max_chunks, a.slot};
-  const int n_attn = M * a.n_head * nsplit, n_dense = (N + 7) / 8;
-  const size_t shm = 256 + (size_t)M * K * sizeof(bf16);
-  // U: 512-column chunks per row in flight, the rows_plan choice for 8-wave R = 1 blocks (<= 8 registers' worth)
-  const int cpr = K / 512;
-  const int u = cpr <= 3 || cpr == 5 || cpr == 8 ? cpr : (cpr % 4 == 0 ? 4 : (cpr % 2 == 0 ? 2 : 1));
-  auto go = [&](auto mc, auto uc) {
-    constexpr int MMc = decltype(mc)::value, Uc = decltype(uc)::value;
-    attn_dense_kernel<MMc, Uc><<<n_attn + n_dense, 512, shm, s>>>(a, pa, (const bf16*)W, M, N, K, ep, nsplit,
-                                                                  n_attn, n_dense, sync);
-  };
-  auto gm = [&](auto uc) {
-    if (M == 1) go(EpiKindC<1>{}, uc);
-    else go(EpiKindC<2>{}, uc);
-  };
-  switch (u) {
-    case 1: gm(EpiKindC<1>{}); break;
-    case 2: gm(EpiKindC<2>{}); break;
-    case 3: gm(EpiKindC<3>{}); break;
-    case 5: gm(EpiKindC<5>{}); break;
-    case 8: gm(EpiKindC<8>{}); break;
-    default: gm(EpiKindC<4>{}); break;
   }
 }
 

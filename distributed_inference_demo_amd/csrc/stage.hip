@@ -118,10 +118,6 @@ struct bs_stage {
   int* ids = nullptr;                  // [T] staging for host ids
   int* past_dev = nullptr;
   unsigned* att_tickets = nullptr;     // [max_batch][n_head]
-  unsigned* fuse_sync = nullptr;       // attn_dense_kernel's 3 words (zero between launches)
-  // BS_ATTN_DENSE=1: split attention + dense GEMV in one launch (attn_dense_kernel).  Off: its in-launch
-  // all-to-all hand-off costs more than the kernel boundary it removes (profiles/r05_attn_dense_ab.txt).
-  bool attn_dense = false;
   std::vector<int> past_next;          // what past_dev[0..B) holds after the enqueued forwards (last stage)
   bool past_next_valid = false;
   hipStream_t past_stream = nullptr;   // the stream those forwards were enqueued on
@@ -588,7 +584,6 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   wadd((size_t)desc->max_batch * desc->n_head * 4);  // attention split-merge tickets
   wadd(kSkCap * 4);                                  // batched-GEMV split-K partials
   wadd(kSkTickets * 4);                              // and their tickets
-  wadd(64);                                          // attn_dense_kernel sync words
   s->wsbytes = woff;
   if (hipMalloc(&s->ws, s->wsbytes) != hipSuccess) return cleanup(fail(BS_ERR_OOM, "workspace allocation failed"));
   int wi = 0;
@@ -609,8 +604,6 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   s->att_tickets = (unsigned*)(s->ws + wo[wi++]);
   s->sk_ws = (float*)(s->ws + wo[wi++]);
   s->sk_tickets = (unsigned*)(s->ws + wo[wi++]);
-  s->fuse_sync = (unsigned*)(s->ws + wo[wi++]);
-  if (const char* ev = std::getenv("BS_ATTN_DENSE")) s->attn_dense = std::atoi(ev) != 0;
   HIP_TRY(hipMemsetAsync(s->ws, 0, s->wsbytes, s->own));
   std::vector<float> sl(desc->n_head);
   alibi_slopes(desc->n_head, sl.data());
@@ -1097,25 +1090,17 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
     // a = x + dense(ctx)
     Epi e2{};
     e2.kind = EPI_RESID; e2.bias = w.t[T_DENSE_B]; e2.out_f32 = s->attn; e2.resid = cur; e2.ldo = h;
-    // B <= 2 with a split context: attention and dense in one launch (attn_dense_kernel); off while a
-    // profiling pass times the attention (3) or GEMV (1) launches on their own
-    const bool fused = a.defer_merge && s->attn_dense && !w.sc[T_DENSE_W] && s->prof.cls != 1 && s->prof.cls != 3 &&
-                       attn_dense_supported(M, h, h, nh, hd, nsplit);
-    if (fused) {
-      launch_attn_dense(a, w.t[T_DENSE_W], M, h, h, e2, s->fuse_sync, st);
+    {
+      ProfScope p(s, st, 3, ctx_sum * nh * hd * 2 * s->esz);
+      launch_attention(s->bf16, a, st);
+    }
+    if (a.defer_merge) {
+      const AttnParts parts{s->part_acc, s->part_ml, nsplit, nh, hd, s->max_chunks, slot};
+      ProfScope p(s, st, 1, w.sc[T_DENSE_W] ? gemv_bytes_q8(s, M, h, h, 4) : gemv_bytes(s, M, h, h, 4));
+      if (w.sc[T_DENSE_W]) launch_linear_q8_parts(parts, (const int8_t*)w.t[T_DENSE_W], w.sc[T_DENSE_W], M, h, h, e2, st);
+      else launch_linear_parts(parts, w.t[T_DENSE_W], M, h, h, e2, st);
     } else {
-      {
-        ProfScope p(s, st, 3, ctx_sum * nh * hd * 2 * s->esz);
-        launch_attention(s->bf16, a, st);
-      }
-      if (a.defer_merge) {
-        const AttnParts parts{s->part_acc, s->part_ml, nsplit, nh, hd, s->max_chunks, slot};
-        ProfScope p(s, st, 1, w.sc[T_DENSE_W] ? gemv_bytes_q8(s, M, h, h, 4) : gemv_bytes(s, M, h, h, 4));
-        if (w.sc[T_DENSE_W]) launch_linear_q8_parts(parts, (const int8_t*)w.t[T_DENSE_W], w.sc[T_DENSE_W], M, h, h, e2, st);
-        else launch_linear_parts(parts, w.t[T_DENSE_W], M, h, h, e2, st);
-      } else {
-        wlinear(s, st, s->ctx, w, T_DENSE_W, M, h, h, with_splitk(s, e2), 4);
-      }
+      wlinear(s, st, s->ctx, w, T_DENSE_W, M, h, h, with_splitk(s, e2), 4);
     }
     // x2 = LN_post(a); g = gelu(x2 W1 + b1)
     Epi e3{};

@@ -61,11 +61,15 @@ def run(name, B, P, K, W=4):
             "prefill_TFLOPs": config.prefill_flops(m, m.n_layer, B, P, True) / tp / 1e12}
 
 
-BATCHED = [("bloom-1b1", 8, 128, 64), ("bloom-1b1", 32, 128, 64), ("bloom-560m", 16, 16, 128), ("bloom-560m", 32, 16, 128),
+BATCHED = [("bloom-1b1", 8, 128, 64), ("bloom-560m", 8, 16, 128), ("bloom-1b1", 32, 128, 64), ("bloom-560m", 16, 16, 128), ("bloom-560m", 32, 16, 128),
            ("bloom-3b", 8, 64, 128), ("bloom-3b", 32, 64, 64), ("bloom-7b1", 16, 128, 64), ("bloom-7b1", 32, 128, 64),
            ("bloom-7b1", 32, 1024, 32)]
 
 if __name__ == "__main__":
     cfgs = CONFIGS[:3] if "--quick" in sys.argv else (BATCHED if "batched" in sys.argv else CONFIGS)
+    only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--only=")]  # --only=bloom-1b1:8,bloom-560m:32
+    if only:
+        keep = {tuple(x.split(":")) for x in only[0].split(",")}
+        cfgs = [c for c in cfgs if (c[0], str(c[1])) in keep]
     for c in cfgs:
         print(json.dumps(run(*c)), flush=True)
