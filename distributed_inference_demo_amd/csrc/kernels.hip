@@ -1203,7 +1203,8 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
 #pragma unroll
     for (int mt = 0; mt < MT; mt++)
 #pragma unroll
-      for (int j = 0; j < KSTEP; j++) xx[mt][j] = *reinterpret_cast<const bf16x8*>(xsrc[mt] + o + 32 * j);
+      for (int j = 0; j < KSTEP; j++)  // B rows past M are never stored: no load (no duplicate activation traffic)
+        xx[mt][j] = mt * 16 + r < M ? *reinterpret_cast<const bf16x8*>(xsrc[mt] + o + 32 * j) : (bf16x8){};
   };
   f32x4 acc[T][MT];
 #pragma unroll
@@ -1239,24 +1240,43 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
         ww[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(src + o));
       }
     };
-#pragma unroll
-    for (int p = 0; p < PD - 1; p++)
-      if (p < LNS) loadw(p, wr[p]);
-    // row min(r, M - 1), columns kbeg + KC * st + 32 j + 8 g .. + 8: this lane's B fragments
-    const float* xrow = ln.x + ((size_t)min(r, M - 1) * ln.row_stride + ln.row_offset) * K;
+    // row r (< M; rows past M are never stored and load nothing), columns kbeg + KC * st + 32 j + 8 g .. + 8: this
+    // lane's B fragments.  gamma / beta of the wave's K part go through LDS once (16 B per lane, 2 x KC x LNS x 2 B
+    // per wave) and are read back as broadcasts, so the block reads them once per wave, not once per B row.
+    // (dead lanes: an offset past the buffer's records -- the load returns 0 and moves no bytes)
+    const bool live = r < M;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(ln.x), (short)0, (int)((((size_t)(M - 1) * ln.row_stride + ln.row_offset) * K + K) * 4), 0x00020000);
+    const uint32_t xoff = live ? (uint32_t)(((size_t)r * ln.row_stride + ln.row_offset) * K * 4) : 0x80000000u;
     float4 xf[LNS][KSTEP][2];
-    u32x4v gr[LNS][KSTEP], br[LNS][KSTEP];
 #pragma unroll
     for (int st = 0; st < LNS; st++)
 #pragma unroll
       for (int j = 0; j < KSTEP; j++) {
-        const int col = kbeg + st * KC + 32 * j + 8 * g;
-        xf[st][j][0] = *reinterpret_cast<const float4*>(xrow + col);
-        xf[st][j][1] = *reinterpret_cast<const float4*>(xrow + col + 4);
-        gr[st][j] = *reinterpret_cast<const u32x4v*>(ln.gamma + col);
-        br[st][j] = *reinterpret_cast<const u32x4v*>(ln.beta + col);
+        const uint32_t col = (uint32_t)(kbeg + st * KC + 32 * j + 8 * g) * 4;
+        xf[st][j][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff + col, 0, 0));
+        xf[st][j][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff + col + 16, 0, 0));
       }
-    const float c = xrow[0];
+    const float c = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, xoff, 0, 0));
+    constexpr int GB = LNS * KC * 2 / 16;  // 16-B pieces of the wave's gamma (and of its beta)
+    constexpr int GI = (2 * GB + 63) / 64;
+    char* gbl = reinterpret_cast<char*>(red + WAVES * (T * 16) * (MT * 16 + 1) + WAVES * 32) + (size_t)w * GB * 32;
+    u32x4v gtmp[GI];
+#pragma unroll
+    for (int it = 0; it < GI; it++) {
+      const int i = min(it * 64 + lane, 2 * GB - 1);
+      gtmp[it] = *reinterpret_cast<const u32x4v*>((i < GB ? ln.gamma : ln.beta) + kbeg + (i % GB) * 8);
+    }
+    // the weight stream goes out behind the activations (loads return in order: waiting for the activations
+    // leaves the weights in flight), every stage of the wave's K part at once when the ring holds them all
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int p = 0; p < PD; p++)
+      if (p < LNS) loadw(p, wr[p]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int it = 0; it < GI; it++)
+      if (it * 64 + lane < 2 * GB) *reinterpret_cast<u32x4v*>(gbl + (it * 64 + lane) * 16) = gtmp[it];
     float a1 = 0.f, a2 = 0.f;
 #pragma unroll
     for (int st = 0; st < LNS; st++)
@@ -1285,10 +1305,13 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
 #pragma unroll
       for (int j = 0; j < KSTEP; j++) {
         float4 g0, g1, b0, b1;
-        bf16x4_to_f32(make_uint2(gr[st][j].x, gr[st][j].y), g0);
-        bf16x4_to_f32(make_uint2(gr[st][j].z, gr[st][j].w), g1);
-        bf16x4_to_f32(make_uint2(br[st][j].x, br[st][j].y), b0);
-        bf16x4_to_f32(make_uint2(br[st][j].z, br[st][j].w), b1);
+        const int pc = (st * KC + 32 * j + 8 * g) / 8;  // 16-B piece of the wave's K part
+        const u32x4v gv = *reinterpret_cast<const u32x4v*>(gbl + pc * 16);
+        const u32x4v bv = *reinterpret_cast<const u32x4v*>(gbl + (GB + pc) * 16);
+        bf16x4_to_f32(make_uint2(gv.x, gv.y), g0);
+        bf16x4_to_f32(make_uint2(gv.z, gv.w), g1);
+        bf16x4_to_f32(make_uint2(bv.x, bv.y), b0);
+        bf16x4_to_f32(make_uint2(bv.z, bv.w), b1);
         const float4 v0 = xf[st][j][0], v1 = xf[st][j][1];
         bf16x8 o;
         o[0] = (bf16)((v0.x - mean) * rstd * g0.x + b0.x); o[1] = (bf16)((v0.y - mean) * rstd * g0.y + b0.y);
@@ -1300,9 +1323,9 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
 #pragma unroll
     for (int st = 0; st < LNS; st++) {
       const int b = st % PD;
-      if (st + PD - 1 < LNS) loadw(st + PD - 1, wr[(st + PD - 1) % PD]);
 #pragma unroll
       for (int i = 0; i < NI; i++) *reinterpret_cast<u32x4v*>(&wl[swz(RPI * i + lr, lc * 16)]) = wr[b][i];
+      if (st + PD < LNS) loadw(st + PD, wr[b]);  // a ring shallower than the K part: refill the slot just staged
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int j = 0; j < KSTEP; j++)
@@ -1346,17 +1369,21 @@ static bool gemv_ldsw4_ln_launch(const LnArgs& ln, const bf16* W, int M, int N, 
   constexpr int WAVES = 8;
   const int nst = K / (WAVES * 64);
   if (M > 16 || K % (WAVES * 64) || nst < 2 || nst > 5) return false;
-  const size_t shm = (size_t)WAVES * T * 16 * 128 + sizeof(float) * WAVES * (T * 16) * 17 + sizeof(float) * WAVES * 32;
+  // weight stages, wave partials, the statistics' exchange, each wave's gamma / beta (2 x nst x 64 x 2 B)
+  const size_t shm = (size_t)WAVES * T * 16 * 128 + sizeof(float) * WAVES * (T * 16) * 17 + sizeof(float) * WAVES * 32 +
+                     (size_t)WAVES * nst * 64 * 4;
   const int blocks = (N + T * 16 - 1) / (T * 16);
   auto go = [&](auto pc, auto lc) {
     constexpr int PDc = decltype(pc)::value, LNSc = decltype(lc)::value;
     gemv_ldsw4_kernel<T, WAVES, 1, bf16, PDc, LNSc><<<blocks, WAVES * 64, shm, s>>>(W, nullptr, M, N, K, ep, ln);
   };
+  // ring = the whole K part (every weight stage in flight behind the activations) while T x stages <= 12 keeps the
+  // kernel spill-free (ISA metadata), else 2 stages
   switch (nst) {
     case 2: go(EpiKindC<2>{}, EpiKindC<2>{}); break;
     case 3: go(EpiKindC<3>{}, EpiKindC<3>{}); break;
-    case 4: go(EpiKindC<2>{}, EpiKindC<4>{}); break;
-    default: go(EpiKindC<3>{}, EpiKindC<5>{}); break;
+    case 4: go(EpiKindC<T <= 3 ? 4 : 2>{}, EpiKindC<4>{}); break;
+    default: go(EpiKindC<T <= 2 ? 5 : 2>{}, EpiKindC<5>{}); break;
   }
   return true;
 }
