@@ -434,6 +434,11 @@ void attn_prefill_tr_launch(const AttnArgs& a, hipStream_t s, int nstg, int pf_t
     const size_t need = (size_t)P * nqt * nspl * QB * (a.head_dim + 4);
     if (need > a.pf_cap || (long)P * nqt > a.pf_ntickets) nspl = 1;
   }
+  // kgroups < 0: two key groups per block (8 waves; each group walks alternate key tiles of the query tile, the
+  // groups merge at the end) when the grid is one unsplit block per CU or fewer and the long query tiles see >= 8
+  // key tiles -- bloom-7b1 / 3b at one row x 512 tokens 16.95 -> 15.8 / 14.7 -> 13.8 us; shorter contexts and
+  // fuller grids are faster with one group (profiles/r05_attn_prefill_ab.txt)
+  if (kgroups < 0) kgroups = (nspl == 1 && (long)nqt * P <= 256 && ktiles >= 8) ? 2 : 1;
   AttnArgs b = a;
   b.pf_tiles = pt;
   const int U = nqt * nspl;

@@ -173,6 +173,9 @@ def test_prefill512_one_row_wide_gemm_tiles(h, nh):
     out_g = gs.forward_host(ids[:, :S], B, S, past_len=0)
     out_o = os_.forward(ids[:, :S], B, S, past_len=0)
     err = check_close(out_g, out_o, "bf16", f"h={h} wide-tile prefill {B}x{S}")
+    # 32 heads x 8 query tiles = one block per CU: the attention runs two key groups per block
+    for t in range(0, S, 64):
+        check_close(out_g[:, t:t + 64], out_o[:, t:t + 64], "bf16", f"h={h} one-row query tile {t // 64}")
     d_g = gs.forward_host(ids[:, S:S + 1], B, 1, past_len=S)
     d_o = os_.forward(ids[:, S:S + 1], B, 1, past_len=S)
     err1 = check_close(d_g, d_o, "bf16", f"h={h} decode after the wide-tile prefill")
