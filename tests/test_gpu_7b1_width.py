@@ -21,7 +21,7 @@ compared with the device's the same way.
 
 configs[3] -- bloom-7b1 micro-batched prefill: a 512-token prefill of B = 2 rows at hd = 128 (h = 4096) and
 hd = 80 (h = 2560, bloom-3b), one layer: eight 64-query tiles under the causal mask, so the MFMA flash
-attention (attn_prefill_mfma_kernel) walks up to eight 64-key tiles per query tile; then one decode step
+attention (attn_prefill_tr_kernel) walks up to eight 64-key tiles per query tile; then one decode step
 over the 512 cached positions.
 """
 import numpy as np

@@ -57,7 +57,7 @@ def test_ldsw4_ragged_tile_columns(B):
 
 @pytest.mark.parametrize("B", [8, 32])
 def test_batched_decode_middle_stage_offset_rows(B):
-    """4 < B <= 32 (ln_rows_wave_kernel + gemv_ldsw4): a 3-layer bloom-1b1-width middle stage fed hidden states
+    """4 < B <= 32 (B <= 16: gemv_ldsw4 with the LayerNorm in its prologue; B > 16: ln_rows_wave_kernel + gemv_ldsw4): a 3-layer bloom-1b1-width middle stage fed hidden states
     with a large common offset (|mean| 20 x std: a plain one-pass sum-of-squares variance would cancel; the
     kernel's shifted sums must not) decodes 3 steps; every output within the wide-block bound."""
     h, nh, L, V = 1536, 16, 4, 2048
@@ -79,7 +79,8 @@ def test_batched_decode_middle_stage_offset_rows(B):
 @pytest.mark.parametrize("h,nh", [(1024, 16), (2560, 32), (4096, 32)])
 @pytest.mark.parametrize("B", [5, 7, 8])
 def test_small_batch_decode_middle_stage_widths(h, nh, B):
-    """4 < B <= 8 at the 560m / 3b / 7b1 widths (ln_rows_wave_kernel + gemv_ldsw4, split-K on the N = h GEMVs): a
+    """4 < B <= 8 at the 560m / 3b / 7b1 widths (gemv_ldsw4 with the LayerNorm in its prologue at 560m / 3b; at 7b1 the
+    K part is 8 stages per wave, beyond the prologue's register budget: ln_rows_wave_kernel first; split-K on the N = h GEMVs): a
     2-layer middle stage fed offset rows at a slot offset decodes 3 steps within the wide-block bound."""
     from test_gpu_parity import check_close
     L, V = 3, 1024
