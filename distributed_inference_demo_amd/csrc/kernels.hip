@@ -1862,14 +1862,22 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
                                                          int M, int N, int K, Epi ep) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass dropped this template's launch stubs (no diagnostic) without it
   constexpr int BM = 128, BN = BN_, BK = 64;
-  constexpr int FJ = BN / 128, WNC = BN / 4;     // 32-column fragments per wave, columns per wave
-  constexpr int NTH = 512;                       // 8 waves: 2 per SIMD, one's MFMAs cover the other's LDS waits
-  constexpr int CA = BM * BK / 8 / NTH, CB = BN * BK / 8 / NTH;  // 16-B chunks per thread per stage: 2, 2 (4)
+  // waves: 2 (M) x WN (N) of 64 x WNC; BN = 128: 8 waves of 64 x 32 (2 per SIMD, one's MFMAs cover the other's LDS
+  // waits); BN = 256: 8 waves of 64 x 64; BN = 96: 6 waves of 64 x 32 (two-thirds of the 128 x 128 block's
+  // staging and fragment reads per step for three-quarters of its MFMAs: more whole tiles where 128 x 128 leaves
+  // CUs idle)
+  constexpr int WN = BN == 256 ? 4 : BN / 32;
+  constexpr int FJ = BN == 256 ? 2 : 1, WNC = BN / WN;  // 32-column fragments per wave, columns per wave
+  constexpr int NTH = 128 * WN;
+  // 16-B chunks per thread per stage (A rounded up to whole wave instructions: the LDS A region is padded so the
+  // extra DMAs land in slots nobody reads, and every wave counts the same DMAs per stage)
+  constexpr int CA = (BM * BK / 8 + NTH - 1) / NTH, CB = BN * BK / 8 / NTH;
+  constexpr int APAD = CA * NTH * 8;             // bf16 elements of a stage's A region
   constexpr int SLD = BN + 8;                    // epilogue staging row stride (floats)
-  constexpr int SMEM = NSTG * (BM + BN) * BK > BM * SLD * 2 ? NSTG * (BM + BN) * BK : BM * SLD * 2;  // + staging
+  constexpr int SMEM = NSTG * (APAD + BN * BK) > BM * SLD * 2 ? NSTG * (APAD + BN * BK) : BM * SLD * 2;  // + staging
   __shared__ __attribute__((aligned(16))) bf16 smem[SMEM];  // 96 KB at 3 stages of 128 x 128, the only LDS object
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 2, wn = w & 3, r = lane & 31, h = lane >> 5;  // wave tile 64 x WNC at (64 wm, WNC wn)
+  const int wm = w / WN, wn = w - wm * WN, r = lane & 31, h = lane >> 5;  // wave tile 64 x WNC at (64 wm, WNC wn)
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM, nk = K / BK;
   const long T = (long)tiles_n * tiles_m * nk;
   const int G = gridDim.x, b = XM ? gemm3_vblock(blockIdx.x, G) : blockIdx.x;
@@ -1879,8 +1887,8 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
   unsigned long long st1 = 0, st2 = 0;
 #endif
   auto sw = [](int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); };
-  auto As = [&](int buf) { return smem + buf * (BM + BN) * BK; };
-  auto Bs = [&](int buf) { return smem + buf * (BM + BN) * BK + BM * BK; };
+  auto As = [&](int buf) { return smem + buf * (APAD + BN * BK); };
+  auto Bs = [&](int buf) { return smem + buf * (APAD + BN * BK) + APAD; };
   // Staging: buffer loads straight into LDS (LDS-DMA, no VGPR round trip), a 32-bit byte offset per lane
   // and the K position as the scalar offset (the host checks M * K and N * K bf16 fit 4 GB).  An LDS-DMA
   // instruction writes 64 consecutive 16-B slots (wave-uniform base + 16 lane), so the XOR swizzle is
@@ -1915,7 +1923,7 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
       const int c = i * NTH + w * 64 + lane, row = c >> 3, ch = (c & 7) ^ ((row >> 1) & 7);
       ob[i] = (uint32_t)(((size_t)min(n0 + row, N - 1) * K + (size_t)k0 * BK + ch * 8) * 2);
     }
-    static_assert(CA * NTH * 8 == BM * BK && CB * NTH * 8 == BN * BK, "every staged chunk has one lane");
+    static_assert(CA * NTH * 8 >= BM * BK && CB * NTH * 8 == BN * BK, "every staged chunk has one lane");
     float bias[FJ], cscale[FJ];
 #pragma unroll
     for (int j = 0; j < FJ; j++) {
@@ -2157,11 +2165,26 @@ static int gemm3_pair_grid(int M, int N, int K, const Epi& ep) {
 
 template <int NSTG = 3, bool XM = true, int BN = 128>
 static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int G) {
+  constexpr int NTH = BN == 256 ? 512 : 128 * (BN / 32);
   switch (ep.kind) {
-    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, NSTG, XM, BN><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
-    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, NSTG, XM, BN><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
-    default: gemm_mfma3_kernel<EPI_GELU, NSTG, XM, BN><<<G, 512, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, NSTG, XM, BN><<<G, NTH, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, NSTG, XM, BN><<<G, NTH, 0, s>>>(x, w, M, N, K, ep); break;
+    default: gemm_mfma3_kernel<EPI_GELU, NSTG, XM, BN><<<G, NTH, 0, s>>>(x, w, M, N, K, ep); break;
   }
+}
+
+// 128 x 96 tiles (6 waves), whole tiles, one per block: where 128 x 128 tiles leave CUs idle (< 200 tiles) and the
+// 128 x 96 grid fills 160..256 CUs with 16..40 K-steps per tile (tools/gemm_splitk_bench.hip, profiles/r05_gemm_n96.txt:
+// bloom-1b1 QKV at 512 tokens 144 tiles of 128 x 128 -> 192 of 128 x 96, 18.8 -> 17.3 us; fc1 20.1 -> 19.7; bloom-3b
+// dense at 1024 tokens 26.7 -> 25.6; long K loses: bloom-7b1 fc2 91 -> 112).  0: not applicable.
+static int gemm3_n96_grid(int M, int N, int K, const Epi& ep) {
+  if (K % 64 || N % 8 || ep.kind == EPI_ARGMAX || K / 64 < 16 || K / 64 > 40) return 0;
+  if (ep.kind == EPI_QKV && ep.head_dim % 8) return 0;
+  if ((size_t)M * K * 2 >= (1ull << 32) || (size_t)N * K * 2 >= (1ull << 32)) return 0;
+  const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+  const long t96 = (long)((M + 127) / 128) * ((N + 95) / 96);
+  if (t128 >= 200 || t96 < 160 || t96 > 256) return 0;
+  return (int)t96;
 }
 
 // gemm_mfma2_kernel with the epilogue kind as a template argument.
@@ -2416,6 +2439,8 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
       gemm3_launch<3, true, 256>(x, w, M, N, K, ep, s, gw);
     } else if (const int gp = gemm3_pair_grid(M, N, K, ep)) {
       gemm3_launch<2>(x, w, M, N, K, ep, s, gp);
+    } else if (const int gn = gemm3_n96_grid(M, N, K, ep)) {
+      gemm3_launch<3, true, 96>(x, w, M, N, K, ep, s, gn);
     } else if (const int g3 = gemm3_grid(M, N, K, ep)) {
       gemm3_launch(x, w, M, N, K, ep, s, g3);
     } else if (blocks(128, 128) >= 240) {

@@ -101,6 +101,25 @@ int main() {
         if (md > 1e-3) printf("           MISMATCH max |diff| %.3g\n", md);
       }
     }
+    if (const int gn = gemm3_n96_grid(M, N, K, ep)) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "m32 128x96 G=%d", gn);
+      const float us = timeit([&] { gemm3_launch<3, true, 96>(X, W, M, N, K, ep, 0, gn); });
+      CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (size_t i = 0; i < ho.size(); i++) md = std::max(md, (double)fabsf(ho[i] - hr[i]));
+      line(nm, us);
+      if (md > 1e-3) printf("           MISMATCH max |diff| %.3g\n", md);
+      for (int g2 : {192, 256}) {  // stream-K over 128 x 96 tiles
+        snprintf(nm, sizeof nm, "m32 128x96 SK G=%d", g2);
+        const float u2 = timeit([&] { gemm3_launch<3, true, 96>(X, W, M, N, K, ep, 0, g2); });
+        CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
+        md = 0;
+        for (size_t i = 0; i < ho.size(); i++) md = std::max(md, (double)fabsf(ho[i] - hr[i]));
+        line(nm, u2);
+        if (md > 1e-3) printf("           MISMATCH max |diff| %.3g\n", md);
+      }
+    }
     if (const int gw = gemm3_wide_grid(M, N, K, ep)) {
       char nm[64];
       snprintf(nm, sizeof nm, "m32 wide 128x256 G=%d", gw);
