@@ -71,6 +71,21 @@ def main():
         dist.all_reduce(x)
     rccl_us = (time.perf_counter() - t0) * 1e6 / 200
     torch.cuda.synchronize()
+    # a matched send + receive of one micro-batch's hidden row, to this rank itself in one group call (RCCL allows
+    # self p2p inside a group): the host cost of the p2p pair an N = 8 rank issues per hop
+    a = torch.zeros(m.hidden, device=dev)
+    b2 = torch.empty_like(a)
+    ops = [dist.P2POp(dist.isend, a, 0), dist.P2POp(dist.irecv, b2, 0)]
+    for w_ in dist.batch_isend_irecv(ops):
+        w_.wait()
+    torch.cuda.synchronize()
+    Stage.stream_delay(cs.cuda_stream, 100000)
+    t0 = time.perf_counter()
+    for _ in range(100):
+        for w_ in dist.batch_isend_irecv(ops):
+            w_.wait()
+    p2p_pair_us = (time.perf_counter() - t0) * 1e6 / 100
+    torch.cuda.synchronize()
     # the pieces of one micro-batch's enqueue (stream busy): torch's current-stream handle, one Stage.forward
     # (Step struct + ctypes + bs_forward's graph launch), and a bare bs_forward with a prebuilt Step
     import ctypes
@@ -100,7 +115,8 @@ def main():
     res = {"shape": f"bloom-1b1 N = 8 stage: 3 layers, {n_mb} one-row micro-batches, vocab slice {m.vocab}",
            "host_us_per_mb": host_mb, "gpu_us_per_mb": gpu_mb, "host_over_gpu": host_mb / gpu_mb,
            "rccl_call_host_us": rccl_us, "current_stream_handle_us": cur_us, "stage_forward_us": fwd_us,
-           "bare_bs_forward_us": raw_us,
+           "bare_bs_forward_us": raw_us, "p2p_send_recv_pair_host_us": p2p_pair_us,
+           "torch_nccl_avoid_record_streams": os.environ.get("TORCH_NCCL_AVOID_RECORD_STREAMS"),
            "n8_middle_rank_rccl_calls_per_mb": 4,
            "modeled_n8_host_us_per_mb": host_mb + 4 * rccl_us,
            "modeled_n8_host_over_gpu": (host_mb + 4 * rccl_us) / gpu_mb}
