@@ -84,9 +84,13 @@ __device__ __forceinline__ float attn_xsum32(float v) {
 // tiles kg, kg + KG, ... with its own LDS ring, and the groups' (m, l, o) meet in LDS at the end -- a split of the keys
 // with no global partials and no ticket, and two waves per SIMD.  KG = 2 halves the serial tile chain of the longest
 // (causal) query tiles.
-template <int NSTG, int HDE, int KG>
+// QG query groups per wave (KG = 1, no key split): a wave takes 16 QG queries, so every K fragment and every
+// transposed V read of a tile feeds QG MFMAs -- half the LDS reads per MFMA at QG = 2 (128-query blocks, for grids
+// with blocks to spare).
+template <int NSTG, int HDE, int KG, int QG = 1>
 __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, int nspl, int U, int xcd_group) {
-  constexpr int KT = 64, QB = 64, TILEB = KT * 256;
+  static_assert(QG == 1 || KG == 1, "query groups with one key group");
+  constexpr int KT = 64, QB = 64 * QG, TILEB = KT * 256;
   constexpr int KSE = HDE / 32, NTE = HDE / 16;
   typedef short s16x4 __attribute__((ext_vector_type(4)));
   typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -139,15 +143,16 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void*)(Vs(st) + (4 * w + i) * 1024), 16, voff[i], so, 0, 0);
   };
   // Q first (older than the DMAs in the wave's vmcnt order, so its wait leaves the tiles in flight)
-  const int q0 = qt * QB + w * 16;
-  bf16x8 qf[KSE];
-  {
-    const int qrow = min(q0 + r, a.S - 1);
+  const int q0 = qt * QB + w * 16 * QG;  // the wave's first query; group j: queries q0 + 16 j + r
+  bf16x8 qf[QG][KSE];
+#pragma unroll
+  for (int j = 0; j < QG; j++) {
+    const int qrow = min(q0 + 16 * j + r, a.S - 1);
     const bf16* qp = (const bf16*)a.q + ((size_t)b * a.S + qrow) * a.hidden + head * hd;
 #pragma unroll
     for (int ks = 0; ks < KSE; ks++) {
       const int d = ks * 32 + 8 * g;
-      qf[ks] = d < hd ? *reinterpret_cast<const bf16x8*>(qp + d) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      qf[j][ks] = d < hd ? *reinterpret_cast<const bf16x8*>(qp + d) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
   // the first tiles are requested at the split's nominal start before past_len is read (it may come from
@@ -162,13 +167,19 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
   const int kstop = nspl > 1 ? min(kbeg + a.pf_tiles * KT, kend) : kend;
   const int ntile = (kstop - kbeg + KT - 1) / KT;
   const int nit = (ntile + KG - 1) / KG;  // loop trips (every group runs them all: the barriers are block-wide)
-  float m_q = -INFINITY, l_q = 0.f;  // running max / sum of query q0 + r (every lane of the query agrees)
-  f32x4 o[NTE];  // o[t][i] = unnormalised context of query q0 + r, dim 16 t + 4 g + i
+  // running max / sum of query q0 + 16 j + r (every lane of the query agrees)
+  float m_q[QG], l_q[QG];
+  f32x4 o[QG][NTE];  // o[j][t][i] = unnormalised context of query q0 + 16 j + r, dim 16 t + 4 g + i
 #pragma unroll
-  for (int t = 0; t < NTE; t++) o[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < QG; j++) {
+    m_q[j] = -INFINITY;
+    l_q[j] = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTE; t++) o[j][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
   const int pg4 = ((g & 1) << 1) | (g >> 1);  // perm(g): this lane group's 4-key block in every 16-key subtile
   const int arow = ((((r >> 2) & 1) << 1) | (r >> 3)) * 4 + (r & 3);  // key (within a subtile) of A row r
-  const int qpos = past + q0 + r;
+  const int qpos = past + q0 + r;  // group j: qpos + 16 j
   const int qq = r >> 2, pp = r & 3;
   for (int it = 0; it < nit; it++) {
     const int st = it % NSTG, ti = it * KG + kg, k0 = kbeg + ti * KT;
@@ -194,65 +205,82 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
 #pragma unroll
       for (int ks = 0; ks < KSE; ks++)
         kf[t][ks] = *reinterpret_cast<const bf16x8*>(ks_ + attn_tr_off(t * 16 + arow, ks * 4 + g));
-    f32x4 sacc[4];
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KSE; ks++) sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][ks], qf[ks], sacc[t], 0, 0, 0);
-    }
-    // scale, ALiBi, causal mask: sacc[t][i] is key k0 + 16 t + 4 perm(g) + i against query q0 + r; the mask only on
-    // the tiles that cross the wave's diagonal or the split's end (wave-uniform test)
-    float sv[4][4], rmax = -INFINITY;
-    const float abase = slope * (float)(k0 + 4 * pg4);
-    const bool full = k0 + KT - 1 <= past + q0 && k0 + KT <= kstop;
+    f32x4 sacc[QG][4];
 #pragma unroll
     for (int t = 0; t < 4; t++)
 #pragma unroll
-      for (int i = 0; i < 4; i++) sv[t][i] = fmaf(a.inv_norm, sacc[t][i], fmaf(slope, (float)(t * 16 + i), abase));
+      for (int j = 0; j < QG; j++) {
+        sacc[j][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KSE; ks++)
+          sacc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][ks], qf[j][ks], sacc[j][t], 0, 0, 0);
+      }
+    // scale, ALiBi, causal mask: sacc[t][i] is key k0 + 16 t + 4 perm(g) + i against query q0 + r; the mask only on
+    // the tiles that cross the wave's diagonal or the split's end (wave-uniform test)
+    float sv[QG][4][4];
+    const float abase = slope * (float)(k0 + 4 * pg4);
+    const bool full = k0 + KT - 1 <= past + q0 && k0 + KT <= kstop;  // (group 0's first query is the earliest)
+#pragma unroll
+    for (int j = 0; j < QG; j++)
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) sv[j][t][i] = fmaf(a.inv_norm, sacc[j][t][i], fmaf(slope, (float)(t * 16 + i), abase));
     if (!full) {
+#pragma unroll
+      for (int j = 0; j < QG; j++)
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int kpos = k0 + t * 16 + 4 * pg4 + i;
+            sv[j][t][i] = (kpos <= qpos + 16 * j && kpos < kstop) ? sv[j][t][i] : -INFINITY;
+          }
+    }
+    float rmax[QG];
+#pragma unroll
+    for (int j = 0; j < QG; j++) {
+      rmax[j] = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) rmax[j] = fmaxf(rmax[j], sv[j][t][i]);
+    }
+    ATTN_STAMP(it, 4);
+#pragma unroll
+    for (int j = 0; j < QG; j++) {
+      rmax[j] = attn_xmax32(attn_xmax16(rmax[j]));
+      const float m_new = fmaxf(m_q[j], rmax[j]);
+      const float scale_q = m_new == -INFINITY ? 1.f : __expf(m_q[j] - m_new);
+      float rs = 0.f;
 #pragma unroll
       for (int t = 0; t < 4; t++)
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-          const int kpos = k0 + t * 16 + 4 * pg4 + i;
-          sv[t][i] = (kpos <= qpos && kpos < kstop) ? sv[t][i] : -INFINITY;
+          const float p = m_new == -INFINITY ? 0.f : __expf(sv[j][t][i] - m_new);
+          sv[j][t][i] = p;
+          rs += p;
         }
+      rs = attn_xsum32(attn_xsum16(rs));
+      l_q[j] = l_q[j] * scale_q + rs;
+      m_q[j] = m_new;
+#pragma unroll
+      for (int t = 0; t < NTE; t++) o[j][t] *= scale_q;
     }
-#pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-      for (int i = 0; i < 4; i++) rmax = fmaxf(rmax, sv[t][i]);
-    ATTN_STAMP(it, 4);
-    rmax = attn_xmax32(attn_xmax16(rmax));
-    const float m_new = fmaxf(m_q, rmax);
-    const float scale_q = m_new == -INFINITY ? 1.f : __expf(m_q - m_new);
-    float rs = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const float p = m_new == -INFINITY ? 0.f : __expf(sv[t][i] - m_new);
-        sv[t][i] = p;
-        rs += p;
-      }
-    rs = attn_xsum32(attn_xsum16(rs));
-    l_q = l_q * scale_q + rs;
-    m_q = m_new;
-#pragma unroll
-    for (int t = 0; t < NTE; t++) o[t] *= scale_q;
     ATTN_STAMP(it, 5);
     // P^T (B operand of step kb): element e = key 32 kb + 16 (e >> 2) + 4 perm(g) + (e & 3) of query r; hi + lo
-    bf16x8 ph[2], pl[2];
+    bf16x8 ph[QG][2], pl[QG][2];
 #pragma unroll
-    for (int kb = 0; kb < 2; kb++)
+    for (int j = 0; j < QG; j++)
 #pragma unroll
-      for (int e = 0; e < 8; e++) {
-        const float p = sv[2 * kb + (e >> 2)][e & 3];
-        const bf16 hi = (bf16)p;
-        ph[kb][e] = hi;
-        pl[kb][e] = (bf16)(p - (float)hi);
-      }
+      for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const float p = sv[j][2 * kb + (e >> 2)][e & 3];
+          const bf16 hi = (bf16)p;
+          ph[j][kb][e] = hi;
+          pl[j][kb][e] = (bf16)(p - (float)hi);
+        }
     ATTN_STAMP(it, 6);
     // V^T fragments by transposed reads: lane 4q + p of group g addresses row (32 kb + 16 h + 4 perm(g) + q), columns
     // 16 t + 4 p .. + 3, and lane r receives column 16 t + r of those 4 rows
@@ -266,8 +294,11 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
         const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (lds_s16x4*)(vs_ + attn_tr_off(rw0 + 16, 2 * t + (pp >> 1)) + 8 * (pp & 1)));
         const bf16x8 vf = __builtin_bit_cast(bf16x8, (s16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, ph[kb], o[t], 0, 0, 0);
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pl[kb], o[t], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < QG; j++) {
+          o[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, ph[j][kb], o[j][t], 0, 0, 0);
+          o[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pl[j][kb], o[j][t], 0, 0, 0);
+        }
       }
   }
   // the clamped DMAs still in flight land before the LDS is reused or the block exits
@@ -277,29 +308,29 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
     __syncthreads();
     float* xm = reinterpret_cast<float*>(smem + NSTG * 2 * TILEB) + (w * 64 + lane) * (NTE * 4 + 2);
     if (kg == 1) {
-      xm[0] = m_q;
-      xm[1] = l_q;
+      xm[0] = m_q[0];
+      xm[1] = l_q[0];
 #pragma unroll
       for (int t = 0; t < NTE; t++)
 #pragma unroll
-        for (int i = 0; i < 4; i++) xm[2 + 4 * t + i] = o[t][i];
+        for (int i = 0; i < 4; i++) xm[2 + 4 * t + i] = o[0][t][i];
     }
     __syncthreads();
     if (kg == 0) {
       const float m1 = xm[0], l1 = xm[1];
-      const float mn = fmaxf(m_q, m1);
-      const float s0 = m_q == -INFINITY ? 0.f : __expf(m_q - mn), s1 = m1 == -INFINITY ? 0.f : __expf(m1 - mn);
-      l_q = l_q * s0 + l1 * s1;
-      m_q = mn;
+      const float mn = fmaxf(m_q[0], m1);
+      const float s0 = m_q[0] == -INFINITY ? 0.f : __expf(m_q[0] - mn), s1 = m1 == -INFINITY ? 0.f : __expf(m1 - mn);
+      l_q[0] = l_q[0] * s0 + l1 * s1;
+      m_q[0] = mn;
 #pragma unroll
       for (int t = 0; t < NTE; t++)
 #pragma unroll
-        for (int i = 0; i < 4; i++) o[t][i] = o[t][i] * s0 + xm[2 + 4 * t + i] * s1;
+        for (int i = 0; i < 4; i++) o[0][t][i] = o[0][t][i] * s0 + xm[2 + 4 * t + i] * s1;
     }
   }
 #ifdef ATTN_STAMPS
   {
-    volatile float sink = o[0][0];  // the P.V MFMAs retired
+    volatile float sink = o[0][0][0];  // the P.V MFMAs retired
     (void)sink;
     if (threadIdx.x == 0 && blockIdx.x < 4096) {
       st_lds[16 * 8 + 1] = __builtin_amdgcn_s_memtime();
@@ -308,7 +339,7 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
     }
   }
 #endif
-  if (nspl > 1) {
+  if (QG == 1 && nspl > 1) {
     // split partial (running max, sum, unnormalised context) of the block's 64 queries, write-through:
     // record [m, l, -, -, o[0..hd)] per (split, query); the block drawing the last ticket of its (row,
     // head, query tile) merges the splits in split order
@@ -320,13 +351,13 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
     const uint32_t rec = (uint32_t)((spl * QB + ql) * rs) * 4;
     if (kg == 0) {
       if (g == 0) {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m_q), rp, rec, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l_q), rp, rec + 4, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m_q[0]), rp, rec, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l_q[0]), rp, rec + 4, 0, 16);
       }
 #pragma unroll
       for (int t = 0; t < NTE; t++) {
         const int d = t * 16 + 4 * g;
-        if (d < hd) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, o[t]), rp, rec + (4 + d) * 4, 0, 16);
+        if (d < hd) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, o[0][t]), rp, rec + (4 + d) * 4, 0, 16);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -398,21 +429,22 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
   // context rows through LDS (the wave's own 16 x 128 bf16 region in group 0's stage 0), then 16-B row stores
   if (kg != 0) return;
   if constexpr (KG == 1) __syncthreads();  // (KG = 2: the merge's barriers already retired every ring read)
-  bf16* cs = reinterpret_cast<bf16*>(smem) + w * 16 * 128;
-  {
-    const float inv = 1.0f / l_q;
+  bf16* cs = reinterpret_cast<bf16*>(smem) + w * 16 * QG * 128;
+#pragma unroll
+  for (int j = 0; j < QG; j++) {
+    const float inv = 1.0f / l_q[j];
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int t = 0; t < NTE; t++) {
       bf16x4 v4;
 #pragma unroll
-      for (int i = 0; i < 4; i++) v4[i] = (bf16)(o[t][i] * inv);
-      *reinterpret_cast<bf16x4*>(cs + r * 128 + t * 16 + 4 * g) = v4;
+      for (int i = 0; i < 4; i++) v4[i] = (bf16)(o[j][t][i] * inv);
+      *reinterpret_cast<bf16x4*>(cs + (16 * j + r) * 128 + t * 16 + 4 * g) = v4;
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes before its reads
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
+  for (int i = 0; i < 4 * QG; i++) {
     const int c = i * 64 + lane, ql = c >> 4, ch = c & 15, q = q0 + ql;
     if (ch < nch && q < a.S)
       *reinterpret_cast<bf16x8*>((bf16*)a.ctx_out + ((size_t)b * a.S + q) * a.hidden + head * hd + ch * 8) =
@@ -422,11 +454,30 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
 
 // Split-KV when the grid would leave CU slots idle: the unit count is nqt x pairs x nspl with nspl = ceil(key tiles
 // / pf_tiles), taken when nqt x pairs < max_units (the blocks co-resident: 2 per CU at 64 KB of LDS); NSTG LDS stages.
-void attn_prefill_tr_launch(const AttnArgs& a, hipStream_t s, int nstg, int pf_tiles, int max_units, int kgroups) {
+void attn_prefill_tr_launch(const AttnArgs& a, hipStream_t s, int nstg, int pf_tiles, int max_units, int kgroups,
+                            int qgroups) {
+  const int P = a.B * a.n_head;
+  // qgroups < 0: two query groups per wave (128-query blocks, half the LDS reads per MFMA) when that grid still has
+  // >= 512 blocks (two per CU) of full query groups; no key split, one key group.  tools/attn_prefill_bench.hip
+  // (profiles/r05_attn_prefill_qg.txt): bloom-7b1 16 rows x 1024 tokens after 1024 cached 1326 -> 840 us, 4 rows x
+  // 1024 tokens 95.8 -> 74.3 us; at 256 blocks (7b1 2 rows x 512) one group is faster (20.8 vs 23.1 us)
+  if (qgroups < 0) qgroups = (a.S >= 128 && (long)((a.S + 127) / 128) * P >= 512) ? 2 : 1;
+  if (qgroups == 2) {
+    const int U2 = (a.S + 127) / 128;
+    const dim3 g2(P * U2);
+    const int xg2 = P % 8 == 0 ? 1 : 0;
+    auto go2 = [&](auto hc) {
+      constexpr int HDE = decltype(hc)::value;
+      attn_prefill_tr_kernel<2, HDE, 1, 2><<<g2, 256, 0, s>>>(a, 1, U2, xg2);
+    };
+    if (a.head_dim <= 64) go2(IntC<64>{});
+    else if (a.head_dim <= 96) go2(IntC<96>{});
+    else go2(IntC<128>{});
+    return;
+  }
   constexpr int QB = 64;
   const int nqt = (a.S + QB - 1) / QB;
   const int ktiles = (a.pf_past_max + a.S + 63) / 64;  // the last query tile's, longest row
-  const int P = a.B * a.n_head;
   const int pt = pf_tiles < 0 ? a.pf_tiles : pf_tiles;
   int nspl = 1;
   if (pt > 0 && a.pf_ws && a.pf_tickets && (long)nqt * P < max_units && ktiles > pt) {

@@ -100,9 +100,10 @@ struct AttnArgs {
 };
 void launch_attention(int is_bf16, const AttnArgs& a, hipStream_t s);
 // S > 1, bf16, head_dim <= 128 (attn_prefill.hip): NSTG LDS stages (2 or 3), split-KV over blocks of pf_tiles key tiles
-// (-1: a.pf_tiles) when the grid has fewer than max_units blocks; kgroups key groups per block (1 or 2; -1: by shape).
+// (-1: a.pf_tiles) when the grid has fewer than max_units blocks; kgroups key groups per block (1 or 2; -1: by shape);
+// qgroups query groups of 16 per wave (1 or 2 = 128-query blocks, no key split; -1: by shape).
 void attn_prefill_tr_launch(const AttnArgs& a, hipStream_t s, int nstg = 2, int pf_tiles = -1, int max_units = 256,
-                            int kgroups = -1);
+                            int kgroups = -1, int qgroups = -1);
 size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, int* max_chunks, int* chunk);
 // Context splits per (row, head) of a decode attention launch (1 = the block writes ctx itself).
 int attention_decode_splits(int B, int n_head, int max_chunks);

@@ -1,4 +1,4 @@
-"""GPU parity of the split-KV prefill attention (kernels.hip attn_prefill_mfma_kernel).
+"""GPU parity of the prefill attention's grid variants (attn_prefill.hip attn_prefill_tr_kernel).
 
 When a prefill's (rows x heads x 64-query tiles) grid is under 256 blocks, each query tile's keys are
 split over blocks of four 64-key tiles whose partial (max, sum, context) records the last-arriving block
@@ -8,7 +8,8 @@ the CPU checker (oracle/bloom_oracle.c, bf16 mode) at the wide-block bound, per 
   * one row, 512 tokens from an empty cache (8 query tiles, 1..8 key tiles, 2 splits);
   * two rows continuing from different cached lengths (130 and 450 positions, per-row bs_step.past_lens):
     row 1's last query tile sees 11 key tiles (3 splits), row 0's at most 6, so its third split is empty;
-  * short prompts (130 tokens: 3 key tiles, one block per query tile) that seed the continuation.
+  * short prompts (130 tokens: 3 key tiles, one block per query tile) that seed the continuation;
+  * many rows (8 x 512 tokens, 16 heads: 512 blocks of 128 queries) -- two 16-query groups per wave.
 """
 import numpy as np
 import pytest
@@ -60,5 +61,28 @@ def test_prefill_split_kv_two_rows_continuing_from_different_lengths(h):
         for t in range(0, S2, 64):
             check_close(yg[r:r + 1, t:t + 64], yo[:, t:t + 64], "bf16", f"h={h} row {r} query tile {t // 64}")
         print(f"h={h} row {r}: continuation {S2} after {lens[r]} max-abs {err:.3e}")
+    gs.close()
+    os_.close()
+
+
+@pytest.mark.parametrize("h", [1024, 1536, 2048])
+def test_prefill_two_query_groups_many_rows(h):
+    """8 rows x 512 tokens (16 heads): 8 x 16 x 4 = 512 blocks of 128 queries, so every wave takes two 16-query
+    groups (each K fragment and transposed V read feeds two MFMAs).  Hidden states per row and per 64-query tile
+    against the checker."""
+    nh, B, S = 16, 8, 512
+    gs = Stage(h, nh, 1, 512, 0, 1, dtype="bf16", max_batch=B, max_ctx=S + 256, max_tokens=B * S, seed=103,
+               is_first=False, is_last=False)
+    os_ = OracleStage(h, nh, 1, 512, 0, 1, bf16=True, max_batch=B, max_ctx=S + 256, seed=103, is_first=False,
+                      is_last=False)
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((B, S, h)).astype(np.float32)
+    yg = gs.forward_host(x, B, S, past_len=0)
+    yo = os_.forward(x, B, S, past_len=0)
+    err = check_close(yg, yo, "bf16", f"h={h} prefill {B}x{S}")
+    for bi in (0, B - 1):
+        for t in range(0, S, 64):
+            check_close(yg[bi:bi + 1, t:t + 64], yo[bi:bi + 1, t:t + 64], "bf16", f"h={h} row {bi} query tile {t // 64}")
+    print(f"h={h}: two-query-group prefill {B}x{S} max-abs {err:.3e}")
     gs.close()
     os_.close()
