@@ -101,6 +101,18 @@ int main() {
         if (md > 1e-3) printf("           MISMATCH max |diff| %.3g\n", md);
       }
     }
+    if (M <= 1024 && N <= 6144) {  // 128 x 96 stream-K at fixed grids on every small shape (round 5)
+      for (int g2 : {128, 192, 256}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "m32 128x96 SKall G=%d", g2);
+        const float u2 = timeit([&] { gemm3_launch<3, true, 96>(X, W, M, N, K, ep, 0, g2); });
+        CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
+        double md = 0;
+        for (size_t i = 0; i < ho.size(); i++) md = std::max(md, (double)fabsf(ho[i] - hr[i]));
+        line(nm, u2);
+        if (md > 1e-3) printf("           MISMATCH max |diff| %.3g\n", md);
+      }
+    }
     if (const int gn = gemm3_n96_grid(M, N, K, ep)) {
       char nm[64];
       snprintf(nm, sizeof nm, "m32 128x96 G=%d", gn);
