@@ -1231,7 +1231,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
     __builtin_amdgcn_wave_barrier();
   };
   if constexpr (LNS > 0) {
-    static_assert(MT == 1 && sizeof(WT) == 2, "LN prologue: one m-tile, bf16 weights");
+    static_assert(sizeof(WT) == 2, "LN prologue: bf16 weights");
     auto loadw = [&](int st, u32x4v (&ww)[NI]) {
       const size_t o = (size_t)st * KC;
 #pragma unroll
@@ -1240,27 +1240,34 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
         ww[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(src + o));
       }
     };
-    // row r (< M; rows past M are never stored and load nothing), columns kbeg + KC * st + 32 j + 8 g .. + 8: this
-    // lane's B fragments.  gamma / beta of the wave's K part go through LDS once (16 B per lane, 2 x KC x LNS x 2 B
-    // per wave) and are read back as broadcasts, so the block reads them once per wave, not once per B row.
+    // rows 16 mt + r (< M; rows past M are never stored and load nothing), columns kbeg + KC * st + 32 j + 8 g .. + 8:
+    // this lane's B fragments.  gamma / beta of the wave's K part go through LDS once (16 B per lane, 2 x KC x LNS x
+    // 2 B per wave) and are read back as broadcasts, so the block reads them once per wave, not once per B row.
     // (dead lanes: an offset past the buffer's records -- the load returns 0 and moves no bytes)
-    const bool live = r < M;
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(ln.x), (short)0, (int)((((size_t)(M - 1) * ln.row_stride + ln.row_offset) * K + K) * 4), 0x00020000);
-    const uint32_t xoff = live ? (uint32_t)(((size_t)r * ln.row_stride + ln.row_offset) * K * 4) : 0x80000000u;
-    float4 xf[LNS][KSTEP][2];
+    uint32_t xoff[MT];
 #pragma unroll
-    for (int st = 0; st < LNS; st++)
+    for (int mt = 0; mt < MT; mt++)
+      xoff[mt] = mt * 16 + r < M ? (uint32_t)(((size_t)(mt * 16 + r) * ln.row_stride + ln.row_offset) * K * 4) : 0x80000000u;
+    float4 xf[MT][LNS][KSTEP][2];
 #pragma unroll
-      for (int j = 0; j < KSTEP; j++) {
-        const uint32_t col = (uint32_t)(kbeg + st * KC + 32 * j + 8 * g) * 4;
-        xf[st][j][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff + col, 0, 0));
-        xf[st][j][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff + col + 16, 0, 0));
-      }
-    const float c = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, xoff, 0, 0));
+    for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+      for (int st = 0; st < LNS; st++)
+#pragma unroll
+        for (int j = 0; j < KSTEP; j++) {
+          const uint32_t col = (uint32_t)(kbeg + st * KC + 32 * j + 8 * g) * 4;
+          xf[mt][st][j][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff[mt] + col, 0, 0));
+          xf[mt][st][j][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff[mt] + col + 16, 0, 0));
+        }
+    float c[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++) c[mt] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, xoff[mt], 0, 0));
     constexpr int GB = LNS * KC * 2 / 16;  // 16-B pieces of the wave's gamma (and of its beta)
     constexpr int GI = (2 * GB + 63) / 64;
-    char* gbl = reinterpret_cast<char*>(red + WAVES * (T * 16) * (MT * 16 + 1) + WAVES * 32) + (size_t)w * GB * 32;
+    float* sred = red + WAVES * (T * 16) * (MT * 16 + 1);  // [WAVES][16 MT rows][2], after the epilogue's area
+    char* gbl = reinterpret_cast<char*>(sred + WAVES * 32 * MT) + (size_t)w * GB * 32;
     u32x4v gtmp[GI];
 #pragma unroll
     for (int it = 0; it < GI; it++) {
@@ -1277,49 +1284,58 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
 #pragma unroll
     for (int it = 0; it < GI; it++)
       if (it * 64 + lane < 2 * GB) *reinterpret_cast<u32x4v*>(gbl + (it * 64 + lane) * 16) = gtmp[it];
-    float a1 = 0.f, a2 = 0.f;
 #pragma unroll
-    for (int st = 0; st < LNS; st++)
+    for (int mt = 0; mt < MT; mt++) {
+      float a1 = 0.f, a2 = 0.f;
 #pragma unroll
-      for (int j = 0; j < KSTEP; j++)
+      for (int st = 0; st < LNS; st++)
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const float d0 = xf[st][j][h].x - c, d1 = xf[st][j][h].y - c, d2 = xf[st][j][h].z - c, d3 = xf[st][j][h].w - c;
-          a1 += (d0 + d1) + (d2 + d3);
-          a2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-        }
-    a1 += __shfl_xor(a1, 16, 64); a1 += __shfl_xor(a1, 32, 64);
-    a2 += __shfl_xor(a2, 16, 64); a2 += __shfl_xor(a2, 32, 64);
-    float* sred = red + WAVES * (T * 16) * (MT * 16 + 1);  // [WAVES][16][2], after the epilogue's area
-    if (g == 0) { sred[(w * 16 + r) * 2] = a1; sred[(w * 16 + r) * 2 + 1] = a2; }
+        for (int j = 0; j < KSTEP; j++)
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const float4 v = xf[mt][st][j][h];
+            const float d0 = v.x - c[mt], d1 = v.y - c[mt], d2 = v.z - c[mt], d3 = v.w - c[mt];
+            a1 += (d0 + d1) + (d2 + d3);
+            a2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+          }
+      a1 += __shfl_xor(a1, 16, 64); a1 += __shfl_xor(a1, 32, 64);
+      a2 += __shfl_xor(a2, 16, 64); a2 += __shfl_xor(a2, 32, 64);
+      if (g == 0) { sred[(w * 16 * MT + mt * 16 + r) * 2] = a1; sred[(w * 16 * MT + mt * 16 + r) * 2 + 1] = a2; }
+    }
     __syncthreads();
-    float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < WAVES; ww++) { t1 += sred[(ww * 16 + r) * 2]; t2 += sred[(ww * 16 + r) * 2 + 1]; }
     const float invk = 1.0f / (float)K;
-    t1 *= invk; t2 *= invk;
-    const float mean = c + t1, rstd = 1.0f / sqrtf(fmaxf(t2 - t1 * t1, 0.f) + ln.eps);
-    bf16x8 xn[LNS][KSTEP];
+    bf16x8 xn[MT][LNS][KSTEP];
 #pragma unroll
-    for (int st = 0; st < LNS; st++)
+    for (int mt = 0; mt < MT; mt++) {
+      float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-      for (int j = 0; j < KSTEP; j++) {
-        float4 g0, g1, b0, b1;
-        const int pc = (st * KC + 32 * j + 8 * g) / 8;  // 16-B piece of the wave's K part
-        const u32x4v gv = *reinterpret_cast<const u32x4v*>(gbl + pc * 16);
-        const u32x4v bv = *reinterpret_cast<const u32x4v*>(gbl + (GB + pc) * 16);
-        bf16x4_to_f32(make_uint2(gv.x, gv.y), g0);
-        bf16x4_to_f32(make_uint2(gv.z, gv.w), g1);
-        bf16x4_to_f32(make_uint2(bv.x, bv.y), b0);
-        bf16x4_to_f32(make_uint2(bv.z, bv.w), b1);
-        const float4 v0 = xf[st][j][0], v1 = xf[st][j][1];
-        bf16x8 o;
-        o[0] = (bf16)((v0.x - mean) * rstd * g0.x + b0.x); o[1] = (bf16)((v0.y - mean) * rstd * g0.y + b0.y);
-        o[2] = (bf16)((v0.z - mean) * rstd * g0.z + b0.z); o[3] = (bf16)((v0.w - mean) * rstd * g0.w + b0.w);
-        o[4] = (bf16)((v1.x - mean) * rstd * g1.x + b1.x); o[5] = (bf16)((v1.y - mean) * rstd * g1.y + b1.y);
-        o[6] = (bf16)((v1.z - mean) * rstd * g1.z + b1.z); o[7] = (bf16)((v1.w - mean) * rstd * g1.w + b1.w);
-        xn[st][j] = o;
+      for (int ww = 0; ww < WAVES; ww++) {
+        t1 += sred[(ww * 16 * MT + mt * 16 + r) * 2];
+        t2 += sred[(ww * 16 * MT + mt * 16 + r) * 2 + 1];
       }
+      t1 *= invk; t2 *= invk;
+      const float mean = c[mt] + t1, rstd = 1.0f / sqrtf(fmaxf(t2 - t1 * t1, 0.f) + ln.eps);
+#pragma unroll
+      for (int st = 0; st < LNS; st++)
+#pragma unroll
+        for (int j = 0; j < KSTEP; j++) {
+          float4 g0, g1, b0, b1;
+          const int pc = (st * KC + 32 * j + 8 * g) / 8;  // 16-B piece of the wave's K part
+          const u32x4v gv = *reinterpret_cast<const u32x4v*>(gbl + pc * 16);
+          const u32x4v bv = *reinterpret_cast<const u32x4v*>(gbl + (GB + pc) * 16);
+          bf16x4_to_f32(make_uint2(gv.x, gv.y), g0);
+          bf16x4_to_f32(make_uint2(gv.z, gv.w), g1);
+          bf16x4_to_f32(make_uint2(bv.x, bv.y), b0);
+          bf16x4_to_f32(make_uint2(bv.z, bv.w), b1);
+          const float4 v0 = xf[mt][st][j][0], v1 = xf[mt][st][j][1];
+          bf16x8 o;
+          o[0] = (bf16)((v0.x - mean) * rstd * g0.x + b0.x); o[1] = (bf16)((v0.y - mean) * rstd * g0.y + b0.y);
+          o[2] = (bf16)((v0.z - mean) * rstd * g0.z + b0.z); o[3] = (bf16)((v0.w - mean) * rstd * g0.w + b0.w);
+          o[4] = (bf16)((v1.x - mean) * rstd * g1.x + b1.x); o[5] = (bf16)((v1.y - mean) * rstd * g1.y + b1.y);
+          o[6] = (bf16)((v1.z - mean) * rstd * g1.z + b1.z); o[7] = (bf16)((v1.w - mean) * rstd * g1.w + b1.w);
+          xn[mt][st][j] = o;
+        }
+    }
 #pragma unroll
     for (int st = 0; st < LNS; st++) {
       const int b = st % PD;
@@ -1332,7 +1348,9 @@ __global__ __launch_bounds__(WAVES * 64) void gemv_ldsw4_kernel(const WT* __rest
 #pragma unroll
         for (int t = 0; t < T; t++) {
           const bf16x8 af = *reinterpret_cast<const bf16x8*>(&wl[swz(t * 16 + r, 64 * j + 16 * g)]);
-          acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, xn[st][j], acc[t][0], 0, 0, 0);
+#pragma unroll
+          for (int mt = 0; mt < MT; mt++)
+            acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, xn[mt][st][j], acc[t][mt], 0, 0, 0);
         }
       __builtin_amdgcn_wave_barrier();
     }
@@ -1363,27 +1381,31 @@ static void gemv_ldsw4_launch(const bf16* X, const WT* W, int M, int N, int K, i
   gemv_ldsw4_kernel<T, WAVES, MT, WT, 2><<<dim3(blocks, KS), WAVES * 64, shm, s>>>(W, X, M, N, K, ep, LnArgs{});
 }
 
-// LN-fused gemv_ldsw4 (bf16, M <= 16, one K split): a wave's K part is K / (8 * 64) stages, 2..5 supported.
+// LN-fused gemv_ldsw4 (bf16, M <= 16, one K split): a wave's K part is K / (8 * 64) stages, 2..5 supported.  (Two
+// m-tiles, 16 < M <= 32, measured slower than the LayerNorm launch + the plain GEMV: bloom-1b1 QKV at M = 32 12.9 vs
+// 2.9 + 7.8 us, decode B = 32 21708 -> 20598 tok/s, profiles/r05_ln_prologue_ab.txt -- the fp32 rows of 32 tokens
+// are twice the bf16 activation bytes the plain GEMV streams.)
 template <int T>
 static bool gemv_ldsw4_ln_launch(const LnArgs& ln, const bf16* W, int M, int N, int K, const Epi& ep, hipStream_t s) {
   constexpr int WAVES = 8;
   const int nst = K / (WAVES * 64);
+  const int mt = 1;
   if (M > 16 || K % (WAVES * 64) || nst < 2 || nst > 5) return false;
   // weight stages, wave partials, the statistics' exchange, each wave's gamma / beta (2 x nst x 64 x 2 B)
-  const size_t shm = (size_t)WAVES * T * 16 * 128 + sizeof(float) * WAVES * (T * 16) * 17 + sizeof(float) * WAVES * 32 +
-                     (size_t)WAVES * nst * 64 * 4;
+  const size_t shm = (size_t)WAVES * T * 16 * 128 + sizeof(float) * WAVES * (T * 16) * (mt * 16 + 1) +
+                     sizeof(float) * WAVES * 32 * mt + (size_t)WAVES * nst * 64 * 4;
   const int blocks = (N + T * 16 - 1) / (T * 16);
-  auto go = [&](auto pc, auto lc) {
-    constexpr int PDc = decltype(pc)::value, LNSc = decltype(lc)::value;
-    gemv_ldsw4_kernel<T, WAVES, 1, bf16, PDc, LNSc><<<blocks, WAVES * 64, shm, s>>>(W, nullptr, M, N, K, ep, ln);
+  auto go = [&](auto mc, auto pc, auto lc) {
+    constexpr int MTc = decltype(mc)::value, PDc = decltype(pc)::value, LNSc = decltype(lc)::value;
+    gemv_ldsw4_kernel<T, WAVES, MTc, bf16, PDc, LNSc><<<blocks, WAVES * 64, shm, s>>>(W, nullptr, M, N, K, ep, ln);
   };
   // ring = the whole K part (every weight stage in flight behind the activations) while T x stages <= 12 keeps the
   // kernel spill-free (ISA metadata), else 2 stages
   switch (nst) {
-    case 2: go(EpiKindC<2>{}, EpiKindC<2>{}); break;
-    case 3: go(EpiKindC<3>{}, EpiKindC<3>{}); break;
-    case 4: go(EpiKindC<T <= 3 ? 4 : 2>{}, EpiKindC<4>{}); break;
-    default: go(EpiKindC<T <= 2 ? 5 : 2>{}, EpiKindC<5>{}); break;
+    case 2: go(EpiKindC<1>{}, EpiKindC<2>{}, EpiKindC<2>{}); break;
+    case 3: go(EpiKindC<1>{}, EpiKindC<3>{}, EpiKindC<3>{}); break;
+    case 4: go(EpiKindC<1>{}, EpiKindC<T <= 3 ? 4 : 2>{}, EpiKindC<4>{}); break;
+    default: go(EpiKindC<1>{}, EpiKindC<T <= 2 ? 5 : 2>{}, EpiKindC<5>{}); break;
   }
   return true;
 }
@@ -1444,7 +1466,7 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
     constexpr int KC = 128 / (int)sizeof(WT);
     if (ln) {
       if constexpr (sizeof(WT) == 2) {
-        if (KS != 1 || two || T > 4) return false;
+        if (KS != 1 || T > 4) return false;
         if (T == 4) return gemv_ldsw4_ln_launch<4>(*ln, w, M, N, K, ep, s);
         if (T == 3) return gemv_ldsw4_ln_launch<3>(*ln, w, M, N, K, ep, s);
         if (T == 2) return gemv_ldsw4_ln_launch<2>(*ln, w, M, N, K, ep, s);
@@ -2370,7 +2392,7 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
     gemv_dispatch<true>(nullptr, ln, (const bf16*)W, M, N, K, ep, s);
     return;
   }
-  if (tiles && M <= 16) {  // LN in the batched GEMV's prologue (gemv_ldsw4 LNS)
+  if (tiles) {  // LN in the batched GEMV's prologue (gemv_ldsw4 LNS) where the shape allows it
     const LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
     if (gemv_tiles_dispatch<bf16>(nullptr, (const bf16*)W, M, N, K, ep, s, &ln)) return;
   }
