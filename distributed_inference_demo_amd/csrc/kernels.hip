@@ -1431,9 +1431,9 @@ static void gemv_tiles_launch(const bf16* X, const WT* W, int M, int N, int K, i
 struct TileCfg { int N, K, T1, KS1, W1, T2, KS2, W2; };  // (T, KS, waves) for M <= 16 and M <= 32
 static const TileCfg kTileTable[] = {
   {3072, 1024, 1, 1, 8, 1, 1, 8},    {1024, 1024, 1, 1, 8, 1, 1, 8},   {4096, 1024, 2, 1, 8, 2, 1, 8},
-  {1024, 4096, 1, 2, 8, 1, 4, 8},
+  {1024, 4096, 1, 1, 8, 1, 4, 8},
   {4608, 1536, 2, 1, 8, 2, 1, 8},    {1536, 1536, 1, 1, 8, 1, 1, 8},   {6144, 1536, 2, 1, 8, 2, 1, 8},
-  {1536, 6144, 2, 4, 8, 2, 4, 8},    {7680, 2560, 2, 1, 8, 2, 1, 8},   {2560, 2560, 1, 1, 8, 1, 1, 8},
+  {1536, 6144, 1, 2, 8, 1, 2, 8},    {7680, 2560, 2, 1, 8, 2, 1, 8},   {2560, 2560, 1, 1, 8, 1, 1, 8},
   {10240, 2560, 3, 1, 8, 3, 1, 8},   {2560, 10240, 2, 2, 8, 2, 5, 8},  {12288, 4096, 3, 1, 8, 3, 1, 8},
   {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 2, 2, 8, 2, 2, 8},
 };
