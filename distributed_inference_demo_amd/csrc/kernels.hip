@@ -750,7 +750,8 @@ __device__ __forceinline__ void emb_rows_finish(const LnArgs& ln, int M, int K, 
 // 2 = no activation loads (x = 1), 4 = no epilogue (a store that never fires keeps the math).
 // Block = blockDim.x / 64 waves (1..16): the dispatch sizes blocks so the grid is ~one block per CU
 // and every CU streams the same number of weight bytes (gemv_rows_dispatch).
-// The block body, shared with attn_dense_kernel: block `bid`.  wait != nullptr (X_PARTS in attn_dense_kernel): the
+// The block body, also used by tools/attn_dense_fused.hip's one-launch attention + dense experiment (measured slower,
+// not in the library; the library always passes wait = nullptr): block `bid`.  wait != nullptr (X_PARTS there): the
 // split-attention partials come from the SAME launch -- the weight stream is issued first, then one lane polls *wait
 // (sc1 loads) until it reaches `target` (bounded: ~0.2 s, then wait[2] = 1 records the timeout), the block meets
 // at a barrier, and every partial load is an sc1 load (MI355X_MICROARCH.md "Valid forms" row 1).
@@ -2502,7 +2503,8 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
 // ticket of its (row, head) merges all partials (sc1 loads, issued together) and writes ctx —
 // MI355X_MICROARCH.md "Valid forms" row 1 (counter form, the last adder reads).
 
-// The block body, shared with attn_dense_kernel: block (head, b, sp) of nsplit.  `done` (attn_dense_kernel): the
+// The block body, also used by tools/attn_dense_fused.hip (the library passes done = nullptr): block (head, b, sp)
+// of nsplit.  `done` (that experiment): the
 // partials go out write-through (sc1) and, after every wave's stores drained, one lane adds 1 to *done (agent
 // scope) -- MI355X_MICROARCH.md "Valid forms" row 1 (ONE lane of each storing workgroup, sc1 payload both sides).
 template <typename T, int WV, int CH>
@@ -2631,7 +2633,7 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, int head, i
   const size_t pair = (size_t)(a.slot + b) * a.n_head + head;
   float* pacc_g = a.part_acc + pair * a.max_chunks * hd;  // [nsplit][hd]
   float* pml_g = a.part_ml + pair * a.max_chunks * 2;     // [nsplit][2]
-  if (done) {  // attn_dense_kernel: the same launch's dense blocks merge (attn_merge.h), sc1 both sides
+  if (done) {  // tools/attn_dense_fused.hip: the same launch's dense blocks merge (attn_merge.h), sc1 both sides
     if (threadIdx.x < hd)
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), attn_rsrc(pacc_g), (uint32_t)(sp * hd + threadIdx.x) * 4, 0, 16);
     if (threadIdx.x == 0) {
