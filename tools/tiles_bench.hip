@@ -19,7 +19,8 @@ int main(int argc, char** argv) {
   struct Sh { const char* name; int N, K; bool ln; } shapes[] = {
       {"1b1 qkv", 4608, 1536, true}, {"1b1 dense", 1536, 1536, false}, {"1b1 fc1", 6144, 1536, true},
       {"1b1 fc2", 1536, 6144, false}, {"560m qkv", 3072, 1024, true}, {"560m dense", 1024, 1024, false},
-      {"560m fc1", 4096, 1024, true}, {"560m fc2", 1024, 4096, false}};
+      {"560m fc1", 4096, 1024, true}, {"560m fc2", 1024, 4096, false}, {"7b1 qkv", 12288, 4096, true},
+      {"7b1 fc1", 16384, 4096, true}};
   const size_t pool_bytes = (size_t)640 << 20;
   char* pool;
   CK(hipMalloc(&pool, pool_bytes));
