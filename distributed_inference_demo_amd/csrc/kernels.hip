@@ -755,10 +755,12 @@ __device__ __forceinline__ void emb_rows_finish(const LnArgs& ln, int M, int K, 
 // split-attention partials come from the SAME launch -- the weight stream is issued first, then one lane polls *wait
 // (sc1 loads) until it reaches `target` (bounded: ~0.2 s, then wait[2] = 1 records the timeout), the block meets
 // at a barrier, and every partial load is an sc1 load (MI355X_MICROARCH.md "Valid forms" row 1).
-template <int R, int MM, int U, int XM, int FL = 0>
+// SYNC (compile time): only the tool instantiates the in-launch wait; in the library it is compiled out.
+template <int R, int MM, int U, int XM, int FL = 0, bool SYNC = false>
 __device__ __forceinline__ void gemv_rows_block(const bf16* __restrict__ W, const bf16* __restrict__ X, const LnArgs& ln,
                                                 const AttnParts& pa, int M, int N, int K, const Epi& ep, int bid,
                                                 char* smem, unsigned* wait, unsigned target) {
+  if constexpr (!SYNC) wait = nullptr;  // every poll / sc1 path below folds away
   constexpr bool LN = XM == X_LN;
   BS_STAMP(0);
   float* scratch = reinterpret_cast<float*>(smem);                  // 64 floats
@@ -1392,6 +1394,9 @@ static bool gemv_ldsw4_ln_launch(const LnArgs& ln, const bf16* W, int M, int N, 
   const int nst = K / (WAVES * 64);
   const int mt = 1;
   if (M > 16 || K % (WAVES * 64) || nst < 2 || nst > 5) return false;
+  // the activation descriptor's byte size and the per-row offsets are 32-bit: rows that reach 2^31 bytes (a long
+  // lm_head row stride) take the LayerNorm launch instead
+  if ((size_t)((size_t)(M - 1) * ln.row_stride + ln.row_offset + 1) * K * 4 >= ((size_t)1 << 31)) return false;
   // weight stages, wave partials, the statistics' exchange, each wave's gamma / beta (2 x nst x 64 x 2 B)
   const size_t shm = (size_t)WAVES * T * 16 * 128 + sizeof(float) * WAVES * (T * 16) * (mt * 16 + 1) +
                      sizeof(float) * WAVES * 32 * mt + (size_t)WAVES * nst * 64 * 4;
@@ -2507,9 +2512,10 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
 // of nsplit.  `done` (that experiment): the
 // partials go out write-through (sc1) and, after every wave's stores drained, one lane adds 1 to *done (agent
 // scope) -- MI355X_MICROARCH.md "Valid forms" row 1 (ONE lane of each storing workgroup, sc1 payload both sides).
-template <typename T, int WV, int CH>
+template <typename T, int WV, int CH, bool SYNC = false>  // SYNC: the tool's `done` counter (compiled out otherwise)
 __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, int head, int b, int sp, int nsplit,
                                                   unsigned* done) {
+  if constexpr (!SYNC) done = nullptr;
   constexpr int NI = CH / 4;  // load instructions per chunk (4 rows each)
   __shared__ __attribute__((aligned(16))) float qs[128];
   __shared__ float es[WV][64];

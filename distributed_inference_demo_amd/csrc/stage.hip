@@ -23,6 +23,21 @@
 
 static thread_local std::string g_err;
 
+// BS_TRACE_CALLS=1: one stderr line (flushed) before each HIP runtime call bs_forward makes, so a host fault inside
+// the runtime names the call it happened in (the round-5 SIGSEGV under rocprofv3).
+static bool trace_calls() {
+  static const bool on = [] { const char* e = getenv("BS_TRACE_CALLS"); return e && e[0] == '1'; }();
+  return on;
+}
+#define BS_TRACE(...)                                         \
+  do {                                                        \
+    if (trace_calls()) {                                      \
+      fprintf(stderr, "[bs_forward] " __VA_ARGS__);           \
+      fputc('\n', stderr);                                    \
+      fflush(stderr);                                         \
+    }                                                         \
+  } while (0)
+
 static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -1231,6 +1246,7 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
     for (int i = 0; i < M; i++)
       if (ids[i] < 0 || ids[i] >= d.vocab) return fail(BS_ERR_INVALID, "token id out of range");
   }
+  BS_TRACE("B=%d S=%d slot=%d flags=%u stream=%p hipSetDevice", B, S, slot, (unsigned)step->flags, stream);
   HIP_TRY(hipSetDevice(d.device));
   hipStream_t st = stream ? (hipStream_t)stream : s->own;
 
@@ -1250,12 +1266,17 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
       if (g.first == key) { exec = g.second; break; }
     if (!exec) {
       hipGraph_t gr = nullptr;
+      BS_TRACE("hipStreamBeginCapture");
       HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+      BS_TRACE("enqueue_forward (capturing)");
       int rc = enqueue_forward(s, step, in, out, logits, st, s->past_dev, pasts);
+      BS_TRACE("hipStreamEndCapture");
       hipError_t ce = hipStreamEndCapture(st, &gr);
       if (rc != BS_OK) { if (gr) hipGraphDestroy(gr); return rc; }
       if (ce != hipSuccess) return fail(BS_ERR_DEVICE, std::string("graph capture: ") + hipGetErrorString(ce));
+      BS_TRACE("hipGraphInstantiate");
       hipError_t ie = hipGraphInstantiate(&exec, gr, nullptr, nullptr, 0);
+      BS_TRACE("hipGraphDestroy");
       hipGraphDestroy(gr);
       if (ie != hipSuccess) return fail(BS_ERR_DEVICE, std::string("graph instantiate: ") + hipGetErrorString(ie));
       if (s->graphs.size() >= 64) {
@@ -1264,13 +1285,22 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
       }
       s->graphs.push_back({key, exec});
     }
-    if (!past_matches) launch_set_past(s->past_dev, pasts.data(), B, st);
+    if (!past_matches) {
+      BS_TRACE("set_past launch");
+      launch_set_past(s->past_dev, pasts.data(), B, st);
+    }
+    BS_TRACE("hipGraphLaunch");
     HIP_TRY(hipGraphLaunch(exec, st));
   } else {
-    if (!past_matches) launch_set_past(s->past_dev, pasts.data(), B, st);
+    if (!past_matches) {
+      BS_TRACE("set_past launch");
+      launch_set_past(s->past_dev, pasts.data(), B, st);
+    }
+    BS_TRACE("enqueue_forward (eager)");
     int rc = enqueue_forward(s, step, in, out, logits, st, s->past_dev, pasts);
     if (rc != BS_OK) return rc;
   }
+  BS_TRACE("hipGetLastError");
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(BS_ERR_DEVICE, std::string("kernel launch: ") + hipGetErrorString(err));
   if (d.is_last) {  // the last kernel advanced past_dev[0..B) by S (stream-ordered before the next forward)
@@ -1279,6 +1309,10 @@ extern "C" int bs_forward(bs_stage* s, const bs_step* step, const void* in, void
     s->past_next_valid = true;
     s->past_stream = st;
   }
-  if (host_io) HIP_TRY(hipStreamSynchronize(st));
+  if (host_io) {
+    BS_TRACE("hipStreamSynchronize");
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  BS_TRACE("done");
   return BS_OK;
 }

@@ -237,6 +237,10 @@ class Pipeline:
                 self._head_role(j, record)
             self.past[j] = [p + seq for p in self.past[j]] if isinstance(self.past[j], list) else self.past[j] + seq
         self.tokens_held = False
+        if hasattr(self.ex, "set_stream"):
+            # the handle is this round's: a later prefill_row (or a caller that switched streams) looks the current
+            # stream up again, so its forward stays ordered with its own receive and send
+            self.ex.set_stream(None)
 
     def prefill_row(self, j, r, ids, n):
         """One pipeline pass of row r of micro-batch j alone: its n prompt tokens at positions 0..n-1 of KV slot

@@ -211,7 +211,10 @@ void or_set_accum_mode(int mode) { g_accum_mode = mode; }
 /* test knob (bit mask) for the P.V product of the attention, emulating device roundings the bf16 mode does
  * not model: 1 = V rounded to fp16 (|V| > 65504 -> inf), 2 = P = fp16(p) + fp16(p - fp16(p)), 4 = P =
  * bf16(p) + bf16(p - bf16(p)); with any bit set P is exp(s - max) unnormalised and the context is divided
- * by the sum after the product (the device's order).  0: the HF order (normalised p, fp32). */
+ * by the sum after the product (the device's order).  8 = the roundings of bits 1/2/4 apply to S > 1 calls
+ * only (the prefill kernel, attn_prefill.hip); S = 1 calls keep fp32 P, unnormalised, divided after (the
+ * decode kernel's order, kernels.hip attn_decode_block).  4 | 8 models the bf16 device library.
+ * 0: the HF order (normalised p, fp32). */
 static int g_emul_pv = 0;
 void or_set_emul_pv(int mask) { g_emul_pv = mask; }
 /* diagnostic knob: bits of bf16 rounding points to SKIP (1 LN out, 2 K/V, 4 q, 8 ctx, 16 GELU out) */
@@ -352,14 +355,15 @@ int or_forward(or_stage *s, int B, int S, int slot, int past_len, const void *in
           float inv = 1.0f / sum;
           float *o = ctx + (size_t)m * h + (size_t)hh * hd;
           for (int d = 0; d < hd; d++) o[d] = 0.f;
-          if (g_emul_pv) {
+          const int emul = ((g_emul_pv & 8) && S == 1) ? 8 : g_emul_pv;
+          if (emul) {
             for (int j = 0; j < nk; j++) {
               const float *vr = kv_ptr(s, li, 1, slot + b, hh, j);
               float e = sc[j], hi = e, lo = 0.f;
-              if (g_emul_pv & 2) { hi = rf16(e); lo = rf16(e - hi); }
-              else if (g_emul_pv & 4) { hi = gen_bf16_round(e); lo = gen_bf16_round(e - hi); }
+              if (emul & 2) { hi = rf16(e); lo = rf16(e - hi); }
+              else if (emul & 4) { hi = gen_bf16_round(e); lo = gen_bf16_round(e - hi); }
               for (int d = 0; d < hd; d++) {
-                float v = (g_emul_pv & 1) ? rf16(vr[d]) : vr[d];
+                float v = (emul & 1) ? rf16(vr[d]) : vr[d];
                 o[d] += hi * v + lo * v;
               }
             }

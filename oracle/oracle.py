@@ -91,6 +91,11 @@ class checker_mode:
         return False
 
 
+# or_set_emul_pv bits that model the bf16 device library's P.V staging: bf16 hi + lo P against bf16 V, normalised
+# after the product, in the prefill kernel (attn_prefill.hip); fp32 unnormalised P in the decode kernel (S = 1)
+EMUL_DEVICE = 4 | 8
+
+
 def num_threads():
     return lib().or_num_threads()
 
@@ -99,8 +104,9 @@ class OracleStage:
     """CPU checker for one pipeline stage; same call semantics as the product Stage."""
 
     def __init__(self, hidden, n_head, n_layer, vocab, layer_begin, layer_end, *, bf16=False,
-                 max_batch=1, max_ctx=64, seed=0, eps=1e-5, is_first=None, is_last=None, int8=False):
+                 max_batch=1, max_ctx=64, seed=0, eps=1e-5, is_first=None, is_last=None, int8=False, emul_pv=None):
         self.hidden, self.vocab = hidden, vocab
+        self.emul = emul_pv  # None: the global knob as set (checker_mode); else this stage's own P.V mode per call
         self.is_first = layer_begin == 0 if is_first is None else is_first
         self.is_last = layer_end == n_layer if is_last is None else is_last
         self.h = lib().or_create(hidden, n_head, n_layer, vocab, eps, layer_begin, layer_end,
@@ -117,7 +123,14 @@ class OracleStage:
             x = np.ascontiguousarray(x, dtype=np.float32).reshape(B, S, self.hidden)
         logits = np.empty((B, self.vocab), dtype=np.float32) if (self.is_last and want_logits) else None
         out = np.empty(B, dtype=np.int32) if self.is_last else np.empty((B, S, self.hidden), dtype=np.float32)
-        rc = lib().or_forward(self.h, B, S, slot, past_len, _p(x), _p(out), _p(logits))
+        if self.emul is None:
+            rc = lib().or_forward(self.h, B, S, slot, past_len, _p(x), _p(out), _p(logits))
+        else:
+            lib().or_set_emul_pv(self.emul)
+            try:
+                rc = lib().or_forward(self.h, B, S, slot, past_len, _p(x), _p(out), _p(logits))
+            finally:
+                lib().or_set_emul_pv(0)
         if rc != 0:
             raise ValueError(f"or_forward failed rc={rc}")
         return (out, logits) if want_logits else out

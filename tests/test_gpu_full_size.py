@@ -94,29 +94,35 @@ def test_bloom560m_full_fp32_128_greedy_ids_identical():
     o.close()
 
 
-def test_bloom1b1_full_bf16_against_fp32_reference_recorded():
-    """north_star's comparison is against the fp32 reference (inference.cpp:207-215: fp32 ORT, HF
-    modeling_bloom.py:245-310), not the bf16-emulating checker the bounds above use.  At configs[1] (bloom-1b1,
-    24 layers, V = 250880, 512-token prompt) this RECORDS (asserts nothing beyond sanity) the distance from the
-    benchmarked bf16 device path to the non-emulating fp32 checker (fp32 weights, fp32 everywhere):
-      * teacher-forced: 1 prefill + 32 decode steps fed the fp32 checker's tokens, logits max/mean-abs per step;
-      * free-running: 128 greedy tokens, each side feeding back its own; the first step where the ids differ and
-        the fp32 checker's top-2 logit margin there (a small margin = a near-tie the bf16 weights legitimately flip).
-    Records go to $BS_PARITY_LOG (profiles/r05_parity_errors.jsonl)."""
+# bf16 device against the NON-emulating fp32 reference at configs[1] (bloom-1b1, 24 layers, V = 250880, 512-token
+# prompt), fixed from the committed multi-seed study before this test asserted them (tools/fp32ref_study.py,
+# profiles/r06_fp32ref_study.txt: 6 weight/prompt seeds, teacher-forced logits max-abs per step over the prefill and
+# 32 decode steps):
+FP32REF_MAX_TOL = 4.5e-2     # logits max-abs, any teacher-forced step
+FP32REF_MEAN_TOL = 8e-3      # logits mean-abs, any teacher-forced step
+
+
+def bf16_vs_fp32_reference(seed=0, prompt_seed=1234, P=512, STEPS=128, TF=32):
+    """bloom-1b1 full depth: the benchmarked bf16 device path against the fp32 checker with no bf16 emulation
+    (fp32 weights, fp32 everywhere -- the reference's arithmetic, inference.cpp:207-215 fp32 ORT):
+      * teacher-forced (KV row 0): 1 prefill + TF decode steps fed the fp32 reference's tokens, logits max/mean-abs;
+      * free-running (KV row 1): STEPS greedy tokens, each side feeding back its own; the first step where the ids
+        differ and the reference's top-2 margin there.
+    Returns the record (also written to $BS_PARITY_LOG)."""
     import json
     import os
     import torch
     from test_gpu_parity import record_error
     m = config.get("bloom-1b1")
-    P, STEPS, TF = 512, 128, 32
     g = Stage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, m.n_layer, dtype="bf16", max_batch=2,
-              max_ctx=P + STEPS + 1, max_tokens=P, seed=0)
+              max_ctx=P + STEPS + 1, max_tokens=P, seed=seed)
     o = OracleStage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, m.n_layer, bf16=False, max_batch=2,
-                    max_ctx=P + STEPS + 1, seed=0)
-    ids = prompt_ids(1234, 1, P, m.vocab)
+                    max_ctx=P + STEPS + 1, seed=seed)
+    ids = prompt_ids(prompt_seed, 1, P, m.vocab)
     dev = torch.device("cuda", 0)
     cs = torch.cuda.Stream()
     tf_max, tf_mean = [], []
+    kind = "logits bf16 vs fp32 reference"
     with torch.cuda.stream(cs):
         tin = torch.from_numpy(ids).to(dev)
         tok = torch.empty(1, dtype=torch.int32, device=dev)
@@ -126,16 +132,16 @@ def test_bloom1b1_full_bf16_against_fp32_reference_recorded():
         to, lo = o.forward(ids, 1, P, slot=0, want_logits=True)
         torch.cuda.synchronize()
         first_dev, first_ref = int(tok.cpu()[0]), int(to[0])
-        tf_max.append(record_error("1b1 full prefill [bf16 device vs fp32 reference]", lg.cpu().numpy(), lo, 0.0,
-                                   "logits bf16 vs fp32 reference (recorded)"))
+        tf_max.append(record_error(f"1b1 full s{seed} prefill [bf16 device vs fp32 reference]", lg.cpu().numpy(), lo,
+                                   FP32REF_MAX_TOL, kind))
         tf_mean.append(float(np.abs(lg.cpu().numpy() - lo).mean()))
         for step in range(TF):
             tok.copy_(torch.from_numpy(to))
             g.forward(tok, tok, 1, 1, slot=0, past_len=P + step, logits=lg, stream=cs.cuda_stream)
             to, lo = o.forward(to.reshape(1, 1), 1, 1, slot=0, past_len=P + step, want_logits=True)
             torch.cuda.synchronize()
-            tf_max.append(record_error(f"1b1 full decode step {step} [bf16 device vs fp32 reference]",
-                                       lg.cpu().numpy(), lo, 0.0, "logits bf16 vs fp32 reference (recorded)"))
+            tf_max.append(record_error(f"1b1 full s{seed} decode step {step} [bf16 device vs fp32 reference]",
+                                       lg.cpu().numpy(), lo, FP32REF_MAX_TOL, kind))
             tf_mean.append(float(np.abs(lg.cpu().numpy() - lo).mean()))
         # free-running (KV row 1): both sides greedy on their own tokens
         g.forward(tin, tok, 1, P, slot=1, past_len=0, stream=cs.cuda_stream)
@@ -150,19 +156,33 @@ def test_bloom1b1_full_bf16_against_fp32_reference_recorded():
             dtoks.append(int(tok.cpu()[0]))
             rtoks.append(int(rt[0]))
             margins.append(float(np.diff(np.sort(rl[0])[-2:])[0]))
+    g.close()
+    o.close()
     diff = [i for i in range(STEPS) if dtoks[i] != rtoks[i]]
     first = diff[0] if diff else None
-    rec = {"test": "test_bloom1b1_full_bf16_against_fp32_reference_recorded", "kind": "free-running bf16 vs fp32 reference",
-           "steps": STEPS, "identical_prefix": first if first is not None else STEPS, "first_divergence_step": first,
+    rec = {"test": "bf16_vs_fp32_reference", "kind": "free-running bf16 vs fp32 reference", "seed": seed,
+           "prompt_seed": prompt_seed, "steps": STEPS, "identical_prefix": first if first is not None else STEPS,
+           "first_divergence_step": first,
            "ref_top2_margin_at_divergence": margins[first] if first is not None else None,
            "ref_top2_margin_min_before": min(margins[:first]) if first else (min(margins) if first is None else None),
            "teacher_forced_logits_max_abs": {"max": max(tf_max), "median": float(np.median(tf_max))},
-           "teacher_forced_logits_mean_abs_max": max(tf_mean), "first_token_device": first_dev, "first_token_ref": first_ref}
-    print(json.dumps(rec))
+           "teacher_forced_logits_mean_abs_max": max(tf_mean), "first_token_device": first_dev,
+           "first_token_ref": first_ref, "tf_max": tf_max, "tf_mean": tf_mean}
+    print(json.dumps({k: v for k, v in rec.items() if k not in ("tf_max", "tf_mean")}))
     path = os.environ.get("BS_PARITY_LOG")
     if path:
         with open(path, "a") as f:
-            f.write(json.dumps(rec) + "\n")
-    assert all(np.isfinite(tf_max)) and len(dtoks) == STEPS
-    g.close()
-    o.close()
+            f.write(json.dumps({k: v for k, v in rec.items() if k not in ("tf_max", "tf_mean")}) + "\n")
+    return rec
+
+
+def test_bloom1b1_full_bf16_against_fp32_reference():
+    """north_star's own comparison at configs[1]: the bf16 device against the fp32 reference (not the
+    bf16-emulating checker the bounds above use).  Asserted: the 128 free-running greedy ids are IDENTICAL to the
+    fp32 reference's (north_star: "identical greedy token IDs over a fixed 128-token decode"), and every
+    teacher-forced step's logits are within FP32REF_MAX_TOL max-abs / FP32REF_MEAN_TOL mean-abs (constants fixed
+    from the multi-seed study before the assertion was added)."""
+    rec = bf16_vs_fp32_reference(seed=0, prompt_seed=1234)
+    assert rec["first_divergence_step"] is None, rec
+    assert max(rec["tf_max"]) <= FP32REF_MAX_TOL, rec["tf_max"]
+    assert max(rec["tf_mean"]) <= FP32REF_MEAN_TOL, rec["tf_mean"]

@@ -26,20 +26,59 @@ from distributed_inference_demo_amd.stage import (BloomStageError, Stage, create
                                                   run_inference_worker_residual_last_generation)
 from distributed_inference_demo_amd.config import BloomDims
 from oracle import gen_np
-from oracle.oracle import OracleStage
+from oracle.oracle import EMUL_DEVICE, OracleStage
 
 pytestmark = pytest.mark.gpu
 G = os.path.join(os.path.dirname(__file__), "golden")
 BF16_TOL = 2e-2
 FP32_REL = 1e-3
+# bf16 against the checker that also emulates the device's P.V staging (TwinChecker): relative to max|ref| of the
+# checked tensor (logits or hidden states).  Fixed from the round-6 measurement at these small dimensions (DESIGN.md
+# section 2, profiles/r06_parity_errors.jsonl "tight" records); an indexing / masking error in the attention
+# kernels moves these outputs by 1e-3 or more.
+TIGHT_REL = 1e-3
 
 
-def pair(h, nh, L, V, lb, le, dtype, seed=0, max_batch=1, max_ctx=128, max_tokens=0, is_first=None, is_last=None):
+def pair(h, nh, L, V, lb, le, dtype, seed=0, max_batch=1, max_ctx=128, max_tokens=0, is_first=None, is_last=None,
+         twin=False):
+    """Device stage + checker; twin (bf16): the checker is a TwinChecker (default + emulating)."""
     g = Stage(h, nh, L, V, lb, le, dtype=dtype, max_batch=max_batch, max_ctx=max_ctx, max_tokens=max_tokens,
               seed=seed, is_first=is_first, is_last=is_last)
-    o = OracleStage(h, nh, L, V, lb, le, bf16=(dtype == "bf16"), max_batch=max_batch, max_ctx=max_ctx, seed=seed,
-                    is_first=is_first, is_last=is_last)
+    mk = TwinChecker if (twin and dtype == "bf16") else OracleStage
+    o = mk(h, nh, L, V, lb, le, bf16=(dtype == "bf16"), max_batch=max_batch, max_ctx=max_ctx, seed=seed,
+           is_first=is_first, is_last=is_last)
     return g, o
+
+
+class TwinChecker:
+    """The bf16 checker twice, fed the same inputs: in its default order (what the format-noise bounds compare
+    against) and emulating the device's P.V staging (oracle EMUL_DEVICE: bf16 hi + lo P against bf16 V, normalised
+    after the product, in the prefill kernel; fp32 unnormalised P in the decode kernel).  forward() returns the
+    default checker's result; the emulating twin's is kept in .tight (logits when the stage is last, else the
+    hidden states) for check_tight."""
+
+    def __init__(self, *a, **k):
+        self.o = OracleStage(*a, **k)
+        self.t = OracleStage(*a, emul_pv=EMUL_DEVICE, **k)
+        self.tight = None
+
+    def forward(self, x, B, S, slot=0, past_len=0, want_logits=False):
+        r = self.o.forward(x, B, S, slot=slot, past_len=past_len, want_logits=want_logits)
+        t = self.t.forward(x, B, S, slot=slot, past_len=past_len, want_logits=want_logits)
+        self.tight = t[1] if want_logits else t
+        return r
+
+    def close(self):
+        self.o.close()
+        self.t.close()
+
+
+def check_tight(got, ref, what="", rel=TIGHT_REL):
+    """bf16 device against the emulating checker (TwinChecker.tight): max-abs <= rel * max|ref|."""
+    bound = rel * float(np.abs(ref).max())
+    err = record_error(what + " [emulating checker]", got, ref, bound, "tight bf16")
+    assert err <= bound, f"{what}: max-abs {err} > {bound} against the emulating checker"
+    return err
 
 
 def record_error(what, got, ref, bound, kind):
@@ -118,17 +157,22 @@ def test_tiny_fp32_matches_hf_golden_and_greedy_128():
 def test_tiny_stage_splits_match_oracle(dtype):
     g = np.load(os.path.join(G, "tiny_e2e.npz"))
     h, nh, L, V, seed, B, S = (int(v) for v in g["config"])
+    tw = dtype == "bf16"
     for split in (1, 2, 3):
-        g0, o0 = pair(h, nh, L, V, 0, split, dtype, seed, max_batch=B, max_ctx=32)
-        g1, o1 = pair(h, nh, L, V, split, L, dtype, seed, max_batch=B, max_ctx=32)
+        g0, o0 = pair(h, nh, L, V, 0, split, dtype, seed, max_batch=B, max_ctx=32, twin=tw)
+        g1, o1 = pair(h, nh, L, V, split, L, dtype, seed, max_batch=B, max_ctx=32, twin=tw)
         hid_g = g0.forward_host(g["ids"], B, S)
         hid_o = o0.forward(g["ids"], B, S)
         check_close(hid_g, hid_o, dtype, f"stage0 [0,{split})")
+        if tw:
+            check_tight(hid_g, o0.tight, f"stage0 [0,{split})")
         if dtype == "fp32":
             check_close(hid_g, g["layer_out"][split - 1], dtype, "stage0 vs HF")
         tg, lg = g1.forward_host(hid_o, B, S, want_logits=True)
         to, lo = o1.forward(hid_o, B, S, want_logits=True)
         check_logits(lg, lo, dtype, "stage1 logits")
+        if tw:
+            check_tight(lg, o1.tight, f"stage1 [{split},{L}) logits")
         assert np.array_equal(tg, to)
 
 
@@ -137,10 +181,13 @@ def test_tiny_stage_splits_match_oracle(dtype):
 def test_family_block_prefill_and_decode(fam, dtype):
     f = np.load(os.path.join(G, "family_blocks.npz"))
     h, nh, _, V, seed = (int(v) for v in f[fam + "_config"])
-    gs, os_ = pair(h, nh, 1, V, 0, 1, dtype, seed, max_ctx=64, max_tokens=64, is_last=False)
+    tw = dtype == "bf16"
+    gs, os_ = pair(h, nh, 1, V, 0, 1, dtype, seed, max_ctx=64, max_tokens=64, is_last=False, twin=tw)
+    tight = (lambda got, what: check_tight(got, os_.tight, what)) if tw else (lambda got, what: None)
     out_g = gs.forward_host(f[fam + "_ids64"], 1, 64)
     out_o = os_.forward(f[fam + "_ids64"], 1, 64)
     check_close(out_g, out_o, dtype, f"{fam} S=64")
+    tight(out_g, f"{fam} S=64")
     if dtype == "fp32":
         check_close(out_g, f[fam + "_out64"], dtype, f"{fam} S=64 vs HF")
     ids = f[fam + "_ids23"]
@@ -149,9 +196,11 @@ def test_family_block_prefill_and_decode(fam, dtype):
     o7g = gs.forward_host(ids[:, 15:22], 1, 7, past_len=15)
     o7o = os_.forward(ids[:, 15:22], 1, 7, past_len=15)
     check_close(o7g, o7o, dtype, f"{fam} S=7 past=15")
+    tight(o7g, f"{fam} S=7 past=15")
     o1g = gs.forward_host(ids[:, 22:23], 1, 1, past_len=22)
     o1o = os_.forward(ids[:, 22:23], 1, 1, past_len=22)
     check_close(o1g, o1o, dtype, f"{fam} S=1 past=22")
+    tight(o1g, f"{fam} S=1 past=22")
     if dtype == "fp32":
         check_close(o7g, f[fam + "_out7"], dtype, "S=7 vs HF")
         check_close(o1g, f[fam + "_out1"], dtype, "S=1 vs HF")
@@ -161,16 +210,18 @@ def test_family_block_prefill_and_decode(fam, dtype):
 def test_batched_decode_with_slot_offset(B):
     """Rows at a slot offset; B > 16 exercises the two-m-tile GEMV; B*S > 32 the MFMA GEMM."""
     h, nh, L, V = 256, 4, 2, 1024
-    gs, os_ = pair(h, nh, L, V, 0, L, "bf16", seed=3, max_batch=B + 2, max_ctx=40, max_tokens=B * 8)
+    gs, os_ = pair(h, nh, L, V, 0, L, "bf16", seed=3, max_batch=B + 2, max_ctx=40, max_tokens=B * 8, twin=True)
     ids = gen_np.prompt_ids(5, B, 8, V).astype(np.int32)
     tg, lg = gs.forward_host(ids, B, 8, slot=2, past_len=0, want_logits=True)
     to, lo = os_.forward(ids, B, 8, slot=2, past_len=0, want_logits=True)
     check_logits(lg, lo, "bf16", "prefill")
+    check_tight(lg, os_.tight, f"B={B} prefill")
     assert_ids_match(tg, to, lo, "prefill")
     for step in range(4):
         tg, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=2, past_len=8 + step, want_logits=True)
         to, lo = os_.forward(to.reshape(B, 1), B, 1, slot=2, past_len=8 + step, want_logits=True)
         check_logits(lg, lo, "bf16", f"decode step {step}")
+        check_tight(lg, os_.tight, f"B={B} decode step {step}")
         assert_ids_match(tg, to, lo, f"decode step {step}")
 
 
@@ -309,7 +360,8 @@ def test_graph_replayed_decode_matches_oracle_long_context(dtype):
     of 200-330 positions span 4-6 attention chunks, exercising the last-arriver merge."""
     import torch
     h, nh, L, V, B, P = 256, 4, 2, 1024, 3, 200
-    gs, os_ = pair(h, nh, L, V, 0, L, dtype, seed=21, max_batch=B, max_ctx=P + 140, max_tokens=B * P)
+    tw = dtype == "bf16"
+    gs, os_ = pair(h, nh, L, V, 0, L, dtype, seed=21, max_batch=B, max_ctx=P + 140, max_tokens=B * P, twin=tw)
     ids = gen_np.prompt_ids(17, B, P, V).astype(np.int32)
     dev = torch.device("cuda", 0)
     cs = torch.cuda.Stream()
@@ -321,6 +373,8 @@ def test_graph_replayed_decode_matches_oracle_long_context(dtype):
         to, lo = os_.forward(ids, B, P, want_logits=True)
         torch.cuda.synchronize()
         check_logits(lg.cpu().numpy(), lo, dtype, "prefill logits")
+        if tw:
+            check_tight(lg.cpu().numpy(), os_.tight, f"prefill {B}x{P} logits")
         for step in range(130):
             tok.copy_(torch.from_numpy(to))  # teacher-force the oracle's tokens
             gs.forward(tok, tok, B, 1, slot=0, past_len=P + step, logits=lg, stream=cs.cuda_stream)
@@ -328,6 +382,8 @@ def test_graph_replayed_decode_matches_oracle_long_context(dtype):
             if step % 13 == 0 or step == 129:
                 torch.cuda.synchronize()
                 check_logits(lg.cpu().numpy(), lo, dtype, f"decode step {step} (ctx {P + step + 1})")
+                if tw:
+                    check_tight(lg.cpu().numpy(), os_.tight, f"decode step {step} (ctx {P + step + 1})")
 
 
 def test_graph_and_eager_paths_agree_bitwise():
@@ -411,7 +467,7 @@ def test_small_batch_decode_from_empty_cache(B, slot, hd):
     import torch
     nh = 4 if hd != 80 else 8
     h, L, V = nh * hd, 2, 1024
-    gs, os_ = pair(h, nh, L, V, 0, L, "bf16", seed=31, max_batch=slot + B, max_ctx=320, max_tokens=B * 300)
+    gs, os_ = pair(h, nh, L, V, 0, L, "bf16", seed=31, max_batch=slot + B, max_ctx=320, max_tokens=B * 300, twin=True)
     dev = torch.device("cuda", 0)
     cs = torch.cuda.Stream()
     with torch.cuda.stream(cs):
@@ -428,6 +484,7 @@ def test_small_batch_decode_from_empty_cache(B, slot, hd):
             if step in steps:
                 torch.cuda.synchronize()
                 check_logits(lg.cpu().numpy(), lo, "bf16", f"fused decode step {step} (ctx {past + 1})")
+                check_tight(lg.cpu().numpy(), os_.tight, f"hd={hd} fused decode step {step} (ctx {past + 1})")
             to = to_next
             past += 1
 

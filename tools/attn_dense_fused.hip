@@ -28,10 +28,10 @@ __global__ __launch_bounds__(512) void attn_dense_kernel(AttnArgs a, AttnParts p
   const int bid = blockIdx.x;
   if (bid < n_attn) {
     const int head = bid % a.n_head, rest = bid / a.n_head;
-    attn_decode_block<bf16, 8, 32>(a, head, rest % a.B, rest / a.B, nsplit, sync);
+    attn_decode_block<bf16, 8, 32, true>(a, head, rest % a.B, rest / a.B, nsplit, sync);
     return;
   }
-  gemv_rows_block<1, MM, U, X_PARTS>(W, nullptr, LnArgs{}, pa, M, N, K, ep, bid - n_attn, smem, sync,
+  gemv_rows_block<1, MM, U, X_PARTS, 0, true>(W, nullptr, LnArgs{}, pa, M, N, K, ep, bid - n_attn, smem, sync,
                                      (unsigned)n_attn);
   if (threadIdx.x == 0) {  // this lane's poll matched above: the last dense block resets the words
     typedef __attribute__((address_space(1))) unsigned gu32;

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Builds the decode-engine timeline diagnostics (tools/engine_timeline.hip) in the A/B variants that
-# tools/gpu_engine_check.sh runs: slots in flight 8 / 4 / 12, and the loader thinned to 1 / 2 slots in
+# profiles/r04_engine_timeline_ab.txt records (each binary run on the box as
+# `./tools/engine_timeline_<variant>`): slots in flight 8 / 4 / 12, and the loader thinned to 1 / 2 slots in
 # flight while its CU's gather wave sweeps.
 set -e
 cd "$(dirname "$0")/.."
