@@ -76,13 +76,32 @@ def test_batched_decode_middle_stage_offset_rows(B):
     os_.close()
 
 
+# bloom-7b1 width (h = 4096) hidden states of this 2-layer middle stage fed 5 + N(0, 1) rows (max |ref| ~18): constant
+# bounds fixed from the committed multi-seed study (tools/parity_study_hidden.py, profiles/r06_parity_study_h4096_hidden.txt:
+# 16 cases, B = 5 and 8, prefill + 3 decode steps).  Distances to the checker's default fp32 order: the device 0.043-0.064
+# max-abs (mean-abs <= 0.0094), two other correct fp32 orders of the same rounded math 0.037-0.054, the float64 checker
+# 0.032-0.048 -- the rounding noise of bf16 storage in any order; the 2e-2 + 2^-9 max|ref| formula was exceeded by one
+# of the 16 cases (ratio 1.13), so at this width it gives way to:
+H4096_HIDDEN_MAX_TOL = 8e-2   # 1.24x the device's largest distance in the study, 1.5x the CPU orders'
+H4096_HIDDEN_MEAN_TOL = 1.25e-2
+
+
+def check_h4096_hidden(got, ref, what):
+    from test_gpu_parity import record_error
+    err = record_error(what, got, ref, H4096_HIDDEN_MAX_TOL, "hidden bf16 (h=4096 study bound)")
+    mean = float(np.abs(np.asarray(got, np.float64) - ref).mean())
+    assert err <= H4096_HIDDEN_MAX_TOL and mean <= H4096_HIDDEN_MEAN_TOL, f"{what}: max-abs {err} mean-abs {mean}"
+
+
 @pytest.mark.parametrize("h,nh", [(1024, 16), (2560, 32), (4096, 32)])
 @pytest.mark.parametrize("B", [5, 7, 8])
 def test_small_batch_decode_middle_stage_widths(h, nh, B):
     """4 < B <= 8 at the 560m / 3b / 7b1 widths (gemv_ldsw4 with the LayerNorm in its prologue at 560m / 3b; at 7b1 the
     K part is 8 stages per wave, beyond the prologue's register budget: ln_rows_wave_kernel first; split-K on the N = h GEMVs): a
-    2-layer middle stage fed offset rows at a slot offset decodes 3 steps within the wide-block bound."""
-    from test_gpu_parity import check_close
+    2-layer middle stage fed offset rows at a slot offset decodes 3 steps within the wide-block bound (h = 4096: the
+    study's constant bound above)."""
+    from test_gpu_parity import check_close as _cc
+    check_close = (lambda g, o, dt, what: check_h4096_hidden(g, o, what)) if h == 4096 else _cc
     L, V = 3, 1024
     gs, os_ = pair(h, nh, L, V, 1, 3, "bf16", seed=41, max_batch=B + 1, max_ctx=16, max_tokens=B * 4, is_first=False,
                    is_last=False)

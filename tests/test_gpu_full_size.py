@@ -96,10 +96,11 @@ def test_bloom560m_full_fp32_128_greedy_ids_identical():
 
 # bf16 device against the NON-emulating fp32 reference at configs[1] (bloom-1b1, 24 layers, V = 250880, 512-token
 # prompt), fixed from the committed multi-seed study before this test asserted them (tools/fp32ref_study.py,
-# profiles/r06_fp32ref_study.txt: 6 weight/prompt seeds, teacher-forced logits max-abs per step over the prefill and
-# 32 decode steps):
-FP32REF_MAX_TOL = 4.5e-2     # logits max-abs, any teacher-forced step
-FP32REF_MEAN_TOL = 8e-3      # logits mean-abs, any teacher-forced step
+# profiles/r06_fp32ref_study.txt: 4 weight/prompt seeds, teacher-forced logits per step over the prefill and 32 decode
+# steps: max-abs 0.029-0.032, mean-abs 0.0048-0.0050; 128 free-running greedy ids identical on every seed, the
+# reference's smallest top-2 margin 2.0):
+FP32REF_MAX_TOL = 4.5e-2     # logits max-abs, any teacher-forced step (1.4x the study's largest)
+FP32REF_MEAN_TOL = 7.5e-3    # logits mean-abs, any teacher-forced step (1.5x)
 
 
 def bf16_vs_fp32_reference(seed=0, prompt_seed=1234, P=512, STEPS=128, TF=32):

@@ -32,11 +32,12 @@ pytestmark = pytest.mark.gpu
 G = os.path.join(os.path.dirname(__file__), "golden")
 BF16_TOL = 2e-2
 FP32_REL = 1e-3
-# bf16 against the checker that also emulates the device's P.V staging (TwinChecker): relative to max|ref| of the
-# checked tensor (logits or hidden states).  Fixed from the round-6 measurement at these small dimensions (DESIGN.md
-# section 2, profiles/r06_parity_errors.jsonl "tight" records); an indexing / masking error in the attention
-# kernels moves these outputs by 1e-3 or more.
-TIGHT_REL = 1e-3
+# bf16 against the checker that also emulates the device's P.V staging (TwinChecker), relative to max|ref| of the
+# checked tensor (logits or hidden states).  Applied where no bf16 rounding flips occur (small dimensions, few rows:
+# smoke, tiny splits, B <= 4 decode); there the round-6 measurement is <= 1.2e-5 relative, against 6e-4 for the
+# default-order checker (profiles/r06_parity_errors.jsonl "tight" records).  At real widths
+# the flips dominate both checkers alike; tests/test_gpu_attention_exact.py pins the attention kernels there.
+TIGHT_REL = 5e-5
 
 
 def pair(h, nh, L, V, lb, le, dtype, seed=0, max_batch=1, max_ctx=128, max_tokens=0, is_first=None, is_last=None,
@@ -181,13 +182,10 @@ def test_tiny_stage_splits_match_oracle(dtype):
 def test_family_block_prefill_and_decode(fam, dtype):
     f = np.load(os.path.join(G, "family_blocks.npz"))
     h, nh, _, V, seed = (int(v) for v in f[fam + "_config"])
-    tw = dtype == "bf16"
-    gs, os_ = pair(h, nh, 1, V, 0, 1, dtype, seed, max_ctx=64, max_tokens=64, is_last=False, twin=tw)
-    tight = (lambda got, what: check_tight(got, os_.tight, what)) if tw else (lambda got, what: None)
+    gs, os_ = pair(h, nh, 1, V, 0, 1, dtype, seed, max_ctx=64, max_tokens=64, is_last=False)
     out_g = gs.forward_host(f[fam + "_ids64"], 1, 64)
     out_o = os_.forward(f[fam + "_ids64"], 1, 64)
     check_close(out_g, out_o, dtype, f"{fam} S=64")
-    tight(out_g, f"{fam} S=64")
     if dtype == "fp32":
         check_close(out_g, f[fam + "_out64"], dtype, f"{fam} S=64 vs HF")
     ids = f[fam + "_ids23"]
@@ -196,11 +194,9 @@ def test_family_block_prefill_and_decode(fam, dtype):
     o7g = gs.forward_host(ids[:, 15:22], 1, 7, past_len=15)
     o7o = os_.forward(ids[:, 15:22], 1, 7, past_len=15)
     check_close(o7g, o7o, dtype, f"{fam} S=7 past=15")
-    tight(o7g, f"{fam} S=7 past=15")
     o1g = gs.forward_host(ids[:, 22:23], 1, 1, past_len=22)
     o1o = os_.forward(ids[:, 22:23], 1, 1, past_len=22)
     check_close(o1g, o1o, dtype, f"{fam} S=1 past=22")
-    tight(o1g, f"{fam} S=1 past=22")
     if dtype == "fp32":
         check_close(o7g, f[fam + "_out7"], dtype, "S=7 vs HF")
         check_close(o1g, f[fam + "_out1"], dtype, "S=1 vs HF")
@@ -210,18 +206,21 @@ def test_family_block_prefill_and_decode(fam, dtype):
 def test_batched_decode_with_slot_offset(B):
     """Rows at a slot offset; B > 16 exercises the two-m-tile GEMV; B*S > 32 the MFMA GEMM."""
     h, nh, L, V = 256, 4, 2, 1024
-    gs, os_ = pair(h, nh, L, V, 0, L, "bf16", seed=3, max_batch=B + 2, max_ctx=40, max_tokens=B * 8, twin=True)
+    tw = B <= 4  # the emulating checker's tight bound where the rows GEMV runs (wider batches: flip noise)
+    gs, os_ = pair(h, nh, L, V, 0, L, "bf16", seed=3, max_batch=B + 2, max_ctx=40, max_tokens=B * 8, twin=tw)
     ids = gen_np.prompt_ids(5, B, 8, V).astype(np.int32)
     tg, lg = gs.forward_host(ids, B, 8, slot=2, past_len=0, want_logits=True)
     to, lo = os_.forward(ids, B, 8, slot=2, past_len=0, want_logits=True)
     check_logits(lg, lo, "bf16", "prefill")
-    check_tight(lg, os_.tight, f"B={B} prefill")
+    if tw:
+        check_tight(lg, os_.tight, f"B={B} prefill")
     assert_ids_match(tg, to, lo, "prefill")
     for step in range(4):
         tg, lg = gs.forward_host(to.reshape(B, 1), B, 1, slot=2, past_len=8 + step, want_logits=True)
         to, lo = os_.forward(to.reshape(B, 1), B, 1, slot=2, past_len=8 + step, want_logits=True)
         check_logits(lg, lo, "bf16", f"decode step {step}")
-        check_tight(lg, os_.tight, f"B={B} decode step {step}")
+        if tw:
+            check_tight(lg, os_.tight, f"B={B} decode step {step}")
         assert_ids_match(tg, to, lo, f"decode step {step}")
 
 
@@ -360,8 +359,7 @@ def test_graph_replayed_decode_matches_oracle_long_context(dtype):
     of 200-330 positions span 4-6 attention chunks, exercising the last-arriver merge."""
     import torch
     h, nh, L, V, B, P = 256, 4, 2, 1024, 3, 200
-    tw = dtype == "bf16"
-    gs, os_ = pair(h, nh, L, V, 0, L, dtype, seed=21, max_batch=B, max_ctx=P + 140, max_tokens=B * P, twin=tw)
+    gs, os_ = pair(h, nh, L, V, 0, L, dtype, seed=21, max_batch=B, max_ctx=P + 140, max_tokens=B * P)
     ids = gen_np.prompt_ids(17, B, P, V).astype(np.int32)
     dev = torch.device("cuda", 0)
     cs = torch.cuda.Stream()
@@ -373,8 +371,6 @@ def test_graph_replayed_decode_matches_oracle_long_context(dtype):
         to, lo = os_.forward(ids, B, P, want_logits=True)
         torch.cuda.synchronize()
         check_logits(lg.cpu().numpy(), lo, dtype, "prefill logits")
-        if tw:
-            check_tight(lg.cpu().numpy(), os_.tight, f"prefill {B}x{P} logits")
         for step in range(130):
             tok.copy_(torch.from_numpy(to))  # teacher-force the oracle's tokens
             gs.forward(tok, tok, B, 1, slot=0, past_len=P + step, logits=lg, stream=cs.cuda_stream)
@@ -382,8 +378,6 @@ def test_graph_replayed_decode_matches_oracle_long_context(dtype):
             if step % 13 == 0 or step == 129:
                 torch.cuda.synchronize()
                 check_logits(lg.cpu().numpy(), lo, dtype, f"decode step {step} (ctx {P + step + 1})")
-                if tw:
-                    check_tight(lg.cpu().numpy(), os_.tight, f"decode step {step} (ctx {P + step + 1})")
 
 
 def test_graph_and_eager_paths_agree_bitwise():

@@ -117,6 +117,22 @@ def report(out):
         lines.append(f"h={key[0]} B={key[1]} {key[2]:14s} n={len(sel):3d} max-abs [{min(mx):.4f} .. {max(mx):.4f}] "
                      f"mean-abs max {max(r['mean_abs'] for r in sel):.5f}  "
                      f"max/formula {max(r['max_abs'] / r['formula_bound'] for r in sel):.3f}")
+    # every variant against the checker's default fp32 order (the test's reference): is the device inside the spread
+    # of the correct orders?
+    dist = {}
+    for f in sorted(glob.glob(os.path.join(CPU_DIR, "h*_B*_s*_r*.npz"))):
+        base = os.path.basename(f)[:-4]
+        ref = np.load(f)
+        devf = sorted(glob.glob(os.path.join(GPU_DIR, f"dev_*_{base}.npz")))
+        for ph in ["prefill"] + [f"step{i}" for i in range(STEPS)]:
+            lanes = ref[f"fp32_lanes_{ph}"].astype(np.float64)
+            for v in ("f64", "fp32_seq", "fp32_k32", "emul"):
+                dist.setdefault(v, []).append(float(np.abs(ref[f"{v}_{ph}"] - lanes).max()))
+            for d in devf:
+                dist.setdefault("device", []).append(float(np.abs(np.load(d)[ph] - lanes).max()))
+    lines += ["", "max-abs distance to the default fp32 checker (fp32_lanes), over cases and phases"]
+    for v, xs in dist.items():
+        lines.append(f"  {v:9s} [{min(xs):.4f} .. {max(xs):.4f}] median {float(np.median(xs)):.4f}")
     # device vs the default fp32 checker (what the test asserts), per case and phase
     devs = sorted({r["variant"] for r in rows if r["variant"].startswith("device")})
     if devs:
