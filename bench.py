@@ -86,8 +86,11 @@ def pmc_traffic(args, kernel_tag, timeout=240):
                "--no-profile", "--no-pmc", "--no-pipeline-n1", "--model", args.model, "--batch", str(args.batch), "--prompt",
                str(args.prompt), "--dtype", args.dtype, "--seed", str(args.seed),
                "--weights", args.weights]
+        # decode steps launched eagerly under counter collection: rocprofiler-sdk's dispatch interception faulted on
+        # graph-launched kernels (profiles/r06_rocprof_pmc_segv.txt); same kernels, bit-identical results
+        env = dict(os.environ, BS_GRAPHS="0")
         try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
         except subprocess.TimeoutExpired:
             return None, f"rocprofv3 {counter} pass timed out"
         files = [os.path.join(dp, f) for dp, _, fs in os.walk(out) for f in fs
@@ -429,6 +432,9 @@ def main(argv=None):
         res, ranges, model = _pipeline(args)
     else:
         res = bench_single(args)
+        if os.environ.get("BS_DUMP_MAPS"):  # diagnostics: the process's mappings, to symbolise a native fault's frames
+            import shutil
+            shutil.copyfile("/proc/self/maps", os.environ["BS_DUMP_MAPS"])
         if not args.no_pipeline_n1:
             # the N = 1 point of the pipeline curve and its configs records ride on the headline: a failure there
             # (out of memory on a shared GPU, a 7b1-shape error) is reported in the line, never loses it

@@ -181,31 +181,15 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
   const int arow = ((((r >> 2) & 1) << 1) | (r >> 3)) * 4 + (r & 3);  // key (within a subtile) of A row r
   const int qpos = past + q0 + r;  // group j: qpos + 16 j
   const int qq = r >> 2, pp = r & 3;
-  for (int it = 0; it < nit; it++) {
-    const int st = it % NSTG, ti = it * KG + kg, k0 = kbeg + ti * KT;
-    ATTN_STAMP(it, 0);
-    // this wave's DMA of tile it retired (the NSTG - 2 younger tiles stay in flight) -> barrier: every wave's
-    // pieces landed and every wave is done reading the stage the next DMA overwrites
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * (NSTG - 2)) : "memory");
-    ATTN_STAMP(it, 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    ATTN_STAMP(it, 2);
-    // always issue (past the end: a clamped re-read into a free stage) so the counted waits stay exact
-    issue((it + NSTG - 1) % NSTG, min(k0 + (NSTG - 1) * KG * KT, a.max_ctx));
-    ATTN_STAMP(it, 3);
-    if (ti >= ntile) continue;  // this group's share ran out (wave-uniform); it still meets the barriers
+  // S^T = K.Q^T of the tile in stage st: every K fragment of the tile read, then the MFMAs
+  auto kq = [&](int st, f32x4 (&sacc)[QG][4]) {
     const unsigned char* ks_ = Ks(st);
-    const unsigned char* vs_ = Vs(st);
-    // S^T = K.Q^T: every K fragment of the tile read, then the MFMAs
     bf16x8 kf[4][KSE];
 #pragma unroll
     for (int t = 0; t < 4; t++)
 #pragma unroll
       for (int ks = 0; ks < KSE; ks++)
         kf[t][ks] = *reinterpret_cast<const bf16x8*>(ks_ + attn_tr_off(t * 16 + arow, ks * 4 + g));
-    f32x4 sacc[QG][4];
 #pragma unroll
     for (int t = 0; t < 4; t++)
 #pragma unroll
@@ -215,8 +199,11 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
         for (int ks = 0; ks < KSE; ks++)
           sacc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][ks], qf[j][ks], sacc[j][t], 0, 0, 0);
       }
-    // scale, ALiBi, causal mask: sacc[t][i] is key k0 + 16 t + 4 perm(g) + i against query q0 + r; the mask only on
-    // the tiles that cross the wave's diagonal or the split's end (wave-uniform test)
+  };
+  // scale, ALiBi, causal mask, online softmax of the tile at k0 (scores in sacc), then O += P.V from stage st
+  auto softmax_pv = [&](int it, int st, int k0, const f32x4 (&sacc)[QG][4]) {
+    // sacc[t][i] is key k0 + 16 t + 4 perm(g) + i against query q0 + r; the mask only on the tiles that cross the
+    // wave's diagonal or the split's end (wave-uniform test)
     float sv[QG][4][4];
     const float abase = slope * (float)(k0 + 4 * pg4);
     const bool full = k0 + KT - 1 <= past + q0 && k0 + KT <= kstop;  // (group 0's first query is the earliest)
@@ -284,6 +271,7 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
     ATTN_STAMP(it, 6);
     // V^T fragments by transposed reads: lane 4q + p of group g addresses row (32 kb + 16 h + 4 perm(g) + q), columns
     // 16 t + 4 p .. + 3, and lane r receives column 16 t + r of those 4 rows
+    const unsigned char* vs_ = Vs(st);
 #pragma unroll
     for (int t = 0; t < NTE; t++)
 #pragma unroll
@@ -300,6 +288,28 @@ __global__ __launch_bounds__(256 * KG) void attn_prefill_tr_kernel(AttnArgs a, i
           o[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pl[j][kb], o[j][t], 0, 0, 0);
         }
       }
+  };
+  // (Round 6 measured a software-pipelined form of this loop -- three LDS stages, tile it + 1's K.Q^T MFMAs issued
+  // ahead of tile it's softmax -- at 0.95-1.01x on the BLOOM prefill shapes and 0.7x with two query groups, which
+  // then lose their second block per CU: profiles/r06_attn_prefill_sp_ab.txt.  Not kept.)
+  for (int it = 0; it < nit; it++) {
+    const int st = it % NSTG, ti = it * KG + kg, k0 = kbeg + ti * KT;
+    ATTN_STAMP(it, 0);
+    // this wave's DMA of tile it retired (the NSTG - 2 younger tiles stay in flight) -> barrier: every wave's
+    // pieces landed and every wave is done reading the stage the next DMA overwrites
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * (NSTG - 2)) : "memory");
+    ATTN_STAMP(it, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    ATTN_STAMP(it, 2);
+    // always issue (past the end: a clamped re-read into a free stage) so the counted waits stay exact
+    issue((it + NSTG - 1) % NSTG, min(k0 + (NSTG - 1) * KG * KT, a.max_ctx));
+    ATTN_STAMP(it, 3);
+    if (ti >= ntile) continue;  // this group's share ran out (wave-uniform); it still meets the barriers
+    f32x4 sacc[QG][4];
+    kq(st, sacc);
+    softmax_pv(it, st, k0, sacc);
   }
   // the clamped DMAs still in flight land before the LDS is reused or the block exits
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -92,6 +92,11 @@ struct ProfClass {
 constexpr size_t kSkCap = (size_t)1024 * 128 * 128;
 constexpr int kSkTickets = 4096;
 
+static int graphs_default() {
+  const char* e = getenv("BS_GRAPHS");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 struct bs_stage {
   bs_stage_desc d;
   int bf16 = 1;
@@ -149,7 +154,10 @@ struct bs_stage {
   float temperature = 1.f;
   uint64_t sample_seed = 0;
   float* sample_logits = nullptr;   // [max_batch][V] logits the sampler reads (device I/O without logits)
-  int graphs_on = 1;                // bs_set_graphs: decode steps on device buffers replay captured graphs
+  // bs_set_graphs: decode steps on device buffers replay captured graphs.  Initial value: 1, or 0 when BS_GRAPHS=0 is
+  // set (rocprofv3 --pmc runs: rocprofiler-sdk's counter-collection dispatch interception faulted on graph-launched
+  // kernels)
+  int graphs_on = graphs_default();
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }

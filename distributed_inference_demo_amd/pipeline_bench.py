@@ -26,6 +26,8 @@ The counterpart in the reference is the per-device loop of Communication.java:38
 The gloo backend (CPU tensors, a caller-supplied executor factory) runs the same schedule and bookkeeping
 on the host: tests use it with the CPU checker as the stage (tests/bench_checker.py).
 """
+import os
+import sys
 import time
 
 import torch
@@ -71,6 +73,12 @@ def _prompt(rows, P, vocab, dev):
     return torch.from_numpy(prompt_ids(1234, rows, P, vocab)).to(dev)
 
 
+def _progress(msg):
+    """BS_PROGRESS=1: one stderr line per phase (long profiled runs show where they are)."""
+    if os.environ.get("BS_PROGRESS") == "1":
+        print(f"[pipeline_bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def run_pipeline(model, rank, world, dev, *, mb_rows, n_mb, head_split, prompts, steps, warmup, dtype="bf16",
                  seed=0, prof_rounds=0, executor_factory=None, replica=False):
     """Build this rank's stage + Pipeline once, then for each prompt length P in `prompts`: a timed P-token
@@ -84,6 +92,7 @@ def run_pipeline(model, rank, world, dev, *, mb_rows, n_mb, head_split, prompts,
     W, K = warmup, steps
     pmax = max(prompts)
     b_rank, b_world = (0, 1) if replica else (rank, world)
+    _progress(f"{model.name}: build (mb_rows {mb_rows}, n_mb {n_mb}, prompts {list(prompts)})")
     pipe, (lb, le) = build_rank(model, b_rank, b_world, dev, dtype=dtype, mb_rows=mb_rows, n_mb=n_mb,
                                 max_ctx=pmax + W + K + prof_rounds + 2, max_seq=pmax, seed=seed,
                                 head_split=head_split and not replica, executor_factory=executor_factory)
@@ -102,6 +111,7 @@ def run_pipeline(model, rank, world, dev, *, mb_rows, n_mb, head_split, prompts,
         dist.barrier()
         _sync(dev)
         timing = []
+        _progress(f"{model.name}: prefill {P}")
         t0 = time.perf_counter()
         pipe.step(P, prompt=prompt, timing=timing)
         _sync(dev)
@@ -141,6 +151,7 @@ def run_pipeline(model, rank, world, dev, *, mb_rows, n_mb, head_split, prompts,
             ms, n, byts = g
             mine["gemv"] = {"launches": n, "avg_us": ms / n * 1e3, "achieved_GBps": (byts / n) / (ms / n * 1e-3) / 1e9}
         allst = [None] * world
+        _progress(f"{model.name}: decode done, gathering the record")
         dist.all_gather_object(allst, mine)
         if rank == 0:
             out.append(_record(model, world, allst, mb_rows, n_mb, P, W, K, dt, t_pre,
@@ -151,6 +162,7 @@ def run_pipeline(model, rank, world, dev, *, mb_rows, n_mb, head_split, prompts,
     del pipe
     if st_close:
         st_close()
+    _progress(f"{model.name}: closed")
     return out if rank == 0 else None
 
 

@@ -173,7 +173,8 @@ int bs_set_sampling(bs_stage *stage, int32_t top_k, float temperature, uint64_t 
 
 /* Decode steps (S = 1) on device buffers are captured once per shape into a hipGraph and replayed
  * (the default, on = 1); on = 0 launches them eagerly every step (same kernels, same results: for
- * debugging and A/B timing).  Drops captured graphs.  Returns BS_OK. */
+ * debugging and A/B timing).  Drops captured graphs.  Returns BS_OK.  A stage starts with graphs off
+ * when the environment holds BS_GRAPHS=0 at bs_init_stage (rocprofv3 --pmc runs). */
 int bs_set_graphs(bs_stage *stage, int32_t on);
 
 /* Forget the cached positions of one KV row (slot), or of all rows when slot < 0. */

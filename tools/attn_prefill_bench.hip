@@ -430,9 +430,10 @@ int main(int argc, char** argv) {
     std::vector<bf16> ho(on);
     // variants: (stages, key tiles per split, split when units < max_units); the last is the round-4 kernel
     // (round 5, second pass: kg / qg = -1 is the library's choice by shape; qg 2 = two query groups per wave)
-    struct Vr { int nstg, pt, mu, kg, qg; } vars[] = {{2, 4, 256, 1, 1}, {2, 4, 256, 2, 1}, {2, 4, 256, 1, 2},
-                                                    {2, 4, 256, -1, -1}, {2, 4, 512, 1, 1}, {2, 2, 512, 1, 1},
-                                                    {2, 4, 512, 2, 1}, {2, 3, 512, 1, 1}, {0, 4, 256, 1, 1}};
+    // (round 6 also ran a software-pipelined loop here, sp = 1: profiles/r06_attn_prefill_sp_ab.txt, not kept)
+    struct Vr { int nstg, pt, mu, kg, qg; } vars[] = {
+        {2, 4, 256, -1, -1}, {2, 4, 256, 1, 1}, {3, 4, 256, 1, 1}, {2, 2, 512, 1, 1}, {2, 8, 256, 1, 1},
+        {2, 4, 256, 1, 2}, {2, 4, 256, 2, 1}};
     for (int kern = 0; kern < (int)(sizeof(vars) / sizeof(vars[0])); kern++) {
       const Vr vr = vars[kern];
       auto launch = [&]() { if (vr.nstg) attn_prefill_tr_launch(a, 0, vr.nstg, vr.pt, vr.mu, vr.kg, vr.qg); else attn_prefill_mfma_launch<4>(a, 0); };
@@ -465,8 +466,9 @@ int main(int argc, char** argv) {
       for (int tq = 0; tq < sh.S; tq++) flops += 4.0 * (sh.past + tq + 1) * sh.hd;
       flops *= (double)sh.B * sh.nh;
       char nm[32];
-      if (vr.nstg) snprintf(nm, sizeof nm, "tr p%d u%d g%d q%d", vr.pt, vr.mu, vr.kg, vr.qg); else snprintf(nm, sizeof nm, "r4");
-      printf("%-18s B=%d S=%4d past=%4d nh=%2d hd=%3d  %-14s %7.2f us/launch (min %7.2f)  %6.1f TFLOP/s  err/(ulp+1e-3) max %.3f\n",
+      if (vr.nstg) snprintf(nm, sizeof nm, "s%d p%d u%d g%d q%d", vr.nstg, vr.pt, vr.mu, vr.kg, vr.qg);
+      else snprintf(nm, sizeof nm, "r4");
+      printf("%-18s B=%d S=%4d past=%4d nh=%2d hd=%3d  %-20s %7.2f us/launch (min %7.2f)  %6.1f TFLOP/s  err/(ulp+1e-3) max %.3f\n",
              sh.name, sh.B, sh.S, sh.past, sh.nh, sh.hd, nm, t[t.size() / 2], t[0],
              flops / (t[t.size() / 2] * 1e-6) / 1e12, md);
     }

@@ -5,13 +5,15 @@ mkdir -p gpurun_out
 R=$PWD
 export BS_PARITY_LOG=$R/gpurun_out/r6b_parity_errors.jsonl
 rm -f $BS_PARITY_LOG
-timeout -k 10 400 python -u -m pytest tests/test_gpu_attention_exact.py tests/test_gpu_parity.py tests/test_gpu_full_size.py \
+[ -n "$SKIP_TESTS" ] || timeout -k 10 400 python -u -m pytest tests/test_gpu_attention_exact.py tests/test_gpu_parity.py tests/test_gpu_full_size.py \
   "tests/test_gpu_batched_gemv.py::test_small_batch_decode_middle_stage_widths" -q --timeout 300 --timeout-method thread \
   -p no:cacheprovider > gpurun_out/r6b_tests.log 2>&1
 echo "pytest rc $?" >> gpurun_out/r6b_tests.log
-timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r6b_smoke.log 2>&1 || exit 1
+[ -n "$SKIP_TESTS" ] || timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r6b_smoke.log 2>&1 || exit 1
+[ -n "$SKIP_TESTS" ] || timeout -k 10 300 ./tools/attn_prefill_bench > gpurun_out/r6b_attn_prefill_ab.txt 2>&1 || exit 1
 export TMPDIR=/tmp
 export BS_TRACE_CALLS=1
+export BS_DUMP_MAPS=$R/gpurun_out/r6_segv_maps.txt
 rm -rf $R/gpurun_out/r6_segv
 cd /tmp && timeout -k 10 500 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $R/gpurun_out/r6_segv \
   -o pmc --output-format csv -- python3 $R/bench.py --cpu-baseline 0 --no-pmc --no-profile --steps 4 --warmup 1 \

@@ -30,6 +30,89 @@ from distributed_inference_demo_amd.pipeline import build_rank, init_distributed
 from distributed_inference_demo_amd.stage import Stage  # noqa: E402
 
 
+def p2p_rounds(st, cs, dev, m, n_mb, past, rounds):
+    """the N = 8 middle rank's per-micro-batch enqueue with its RCCL traffic actually issued on this
+    box.  Per micro-batch: the stage forward (graph replay), then the two hops a middle rank makes -- the hidden row
+    (receive from the previous stage, send to the next) and the packed head-ring message (receive, send) -- each
+    issued here as a matched send + receive addressed to this rank itself on the world-1 nccl group (RCCL pairs a
+    self send with its receive only inside one group call, so each hop is one batch_isend_irecv; the product
+    pipeline's single isend / irecv calls cost less host time each: 'rccl_call_host_us').  Host time per micro-batch
+    with the stream kept busy by a spin, against the GPU time of the same rounds (HIP events).
+    Variant 'graph': forward + both hops of one micro-batch captured into one torch CUDA graph (RCCL in stream
+    capture; the stage launches eagerly into the capture) and replayed, one replay per micro-batch."""
+    h = m.hidden
+    act = [torch.zeros(h, device=dev) for _ in range(n_mb)]
+    act_in = [torch.empty(h, device=dev) for _ in range(n_mb)]
+    ring = [torch.zeros(h // 2 + 8, device=dev) for _ in range(n_mb)]  # [xn bf16 | keys] packed message, as floats
+    ring_in = [torch.empty_like(r) for r in ring]
+    tok = torch.zeros(n_mb, dtype=torch.int32, device=dev)
+
+    def mb(j, pos):
+        st.forward(tok[j:j + 1], tok[j:j + 1], 1, 1, slot=j, past_len=pos, stream=cs.cuda_stream)
+        for w_ in dist.batch_isend_irecv([dist.P2POp(dist.isend, act[j], 0), dist.P2POp(dist.irecv, act_in[j], 0)]):
+            w_.wait()  # stream-level (nccl): the host does not block
+        for w_ in dist.batch_isend_irecv([dist.P2POp(dist.isend, ring[j], 0), dist.P2POp(dist.irecv, ring_in[j], 0)]):
+            w_.wait()
+
+    out = {"p2p_shape": f"per micro-batch: stage forward + 2 self-addressed send/recv pairs ({h * 4} B hidden row, "
+                        f"{(h // 2 + 8) * 4} B ring message), {n_mb} micro-batches per round"}
+    pos = [st.past[j] for j in range(n_mb)]
+    for j in range(n_mb):  # warm-up (connects the self pair)
+        mb(j, pos[j])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    Stage.stream_delay(cs.cuda_stream, 20000)
+    e0.record(cs)
+    for _ in range(rounds):
+        for j in range(n_mb):
+            mb(j, pos[j])
+    e1.record(cs)
+    torch.cuda.synchronize()
+    gpu_mb = e0.elapsed_time(e1) * 1e3 / (rounds * n_mb)
+    Stage.stream_delay(cs.cuda_stream, 200000)
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        for j in range(n_mb):
+            mb(j, pos[j])
+    host_mb = (time.perf_counter() - t0) * 1e6 / (rounds * n_mb)
+    torch.cuda.synchronize()
+    out.update(p2p_eager_host_us_per_mb=host_mb, p2p_eager_gpu_us_per_mb=gpu_mb, p2p_eager_host_over_gpu=host_mb / gpu_mb)
+    # graph variant
+    try:
+        st.set_graphs(False)
+        graphs = []
+        for j in range(n_mb):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cs):
+                mb(j, pos[j])
+            graphs.append(g)
+        torch.cuda.synchronize()
+        for g in graphs:
+            g.replay()
+        torch.cuda.synchronize()
+        Stage.stream_delay(cs.cuda_stream, 20000)
+        e0.record(cs)
+        for _ in range(rounds):
+            for g in graphs:
+                g.replay()
+        e1.record(cs)
+        torch.cuda.synchronize()
+        ggpu = e0.elapsed_time(e1) * 1e3 / (rounds * n_mb)
+        Stage.stream_delay(cs.cuda_stream, 200000)
+        t0 = time.perf_counter()
+        for _ in range(rounds):
+            for g in graphs:
+                g.replay()
+        ghost = (time.perf_counter() - t0) * 1e6 / (rounds * n_mb)
+        torch.cuda.synchronize()
+        out.update(p2p_graph_host_us_per_mb=ghost, p2p_graph_gpu_us_per_mb=ggpu, p2p_graph_host_over_gpu=ghost / ggpu)
+    except Exception as e:  # noqa: BLE001 -- recorded: capture of RCCL p2p refused on this stack
+        out["p2p_graph_error"] = f"{type(e).__name__}: {e}"[:300]
+    finally:
+        st.set_graphs(True)
+    return out
+
+
 def main():
     os.environ.setdefault("MASTER_PORT", "29533")
     os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
@@ -112,6 +195,7 @@ def main():
     raw_us = (time.perf_counter() - t0) * 1e6 / 200
     torch.cuda.synchronize()
     host_mb, gpu_mb = host_ms * 1e3 / n_mb, gpu_ms * 1e3 / n_mb
+    p2p = p2p_rounds(st, cs, dev, m, n_mb, past, rounds) if os.environ.get("P2P", "1") == "1" else {}
     res = {"shape": f"bloom-1b1 N = 8 stage: 3 layers, {n_mb} one-row micro-batches, vocab slice {m.vocab}",
            "host_us_per_mb": host_mb, "gpu_us_per_mb": gpu_mb, "host_over_gpu": host_mb / gpu_mb,
            "rccl_call_host_us": rccl_us, "current_stream_handle_us": cur_us, "stage_forward_us": fwd_us,
@@ -119,7 +203,7 @@ def main():
            "torch_nccl_avoid_record_streams": os.environ.get("TORCH_NCCL_AVOID_RECORD_STREAMS"),
            "n8_middle_rank_rccl_calls_per_mb": 4,
            "modeled_n8_host_us_per_mb": host_mb + 4 * rccl_us,
-           "modeled_n8_host_over_gpu": (host_mb + 4 * rccl_us) / gpu_mb}
+           "modeled_n8_host_over_gpu": (host_mb + 4 * rccl_us) / gpu_mb, **p2p}
     print(json.dumps(res))
     pipe.ex.stage.close()
     dist.destroy_process_group()

@@ -1,5 +1,6 @@
 """MFMA utilisation of the prefill GEMMs from PMC counters (one rocprofv3 --pmc pass per counter set).
 
+    export BS_GRAPHS=0   # eager decode steps under counter collection (profiles/r06_rocprof_pmc_segv.txt)
     cd /tmp && rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d OUT -o pmc \
         --output-format csv -- python3 bench.py --cpu-baseline 0 --no-pmc --no-profile --steps 4 --warmup 1
     python tools/pmc_mfma.py OUT
