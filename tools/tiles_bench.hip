@@ -20,7 +20,9 @@ int main(int argc, char** argv) {
       {"1b1 qkv", 4608, 1536, true}, {"1b1 dense", 1536, 1536, false}, {"1b1 fc1", 6144, 1536, true},
       {"1b1 fc2", 1536, 6144, false}, {"560m qkv", 3072, 1024, true}, {"560m dense", 1024, 1024, false},
       {"560m fc1", 4096, 1024, true}, {"560m fc2", 1024, 4096, false}, {"7b1 qkv", 12288, 4096, true},
-      {"7b1 fc1", 16384, 4096, true}};
+      {"7b1 fc1", 16384, 4096, true}, {"7b1 dense", 4096, 4096, false}, {"7b1 fc2", 4096, 16384, false},
+      {"3b qkv", 7680, 2560, true}, {"3b dense", 2560, 2560, false}, {"3b fc1", 10240, 2560, true},
+      {"3b fc2", 2560, 10240, false}};
   const size_t pool_bytes = (size_t)640 << 20;
   char* pool;
   CK(hipMalloc(&pool, pool_bytes));
@@ -39,8 +41,10 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  const char* only = argc > 1 ? argv[1] : nullptr;
-  for (int M : {8, 32}) {
+  const char* only = argc > 1 && strcmp(argv[1], "all") ? argv[1] : nullptr;  // tiles_bench [shape filter|all] [M]
+  const int mlist[3] = {8, 16, 32};
+  for (int M : mlist) {
+    if (argc > 2 && M != atoi(argv[2])) continue;
     for (auto& sh : shapes) {
       if (only && !strstr(sh.name, only)) continue;
       const size_t wb = (size_t)sh.N * sh.K * 2;
