@@ -1885,11 +1885,16 @@ __host__ __device__ __forceinline__ int gemm3_vblock(int i, int G) { return G % 
 // NSTG LDS stages: 3 (one block per CU) or 2 (two per CU at BN = 128).  BN_ = 128: 8 waves of 64 x 32; BN_ = 256
 // (wide tiles for wide N: bloom-7b1's QKV / fc1 at 512 tokens are 192 / 256 whole 128 x 256 tiles, one per CU, no
 // partial tiles, a third less staging per MFMA): 8 waves of 64 x 64, 144 KB of LDS.
-template <int EK, int NSTG = 3, bool XM = true, int BN_ = 128>
+// BM_ = 256 (with BN_ = 256, round 6): 256 x 256 tiles for the large prefills (configs[4]'s 16 rows x up to 2048 tokens),
+// 8 waves of 128 x 64 -- half the LDS fragment reads per MFMA of the 128-row tiles; two LDS stages (128 KB), the
+// epilogue staged in four 64-row passes.
+template <int EK, int NSTG = 3, bool XM = true, int BN_ = 128, int BM_ = 128>
 __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                                          int M, int N, int K, Epi ep) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass dropped this template's launch stubs (no diagnostic) without it
-  constexpr int BM = 128, BN = BN_, BK = 64;
+  constexpr int BM = BM_, BN = BN_, BK = 64;
+  static_assert(BM == 128 || (BM == 256 && BN == 256), "256-row tiles come with 256 columns");
+  constexpr int FI = BM / 64;  // 32-row fragments per wave (the wave's rows: BM / 2)
   // waves: 2 (M) x WN (N) of 64 x WNC; BN = 128: 8 waves of 64 x 32 (2 per SIMD, one's MFMAs cover the other's LDS
   // waits); BN = 256: 8 waves of 64 x 64; BN = 96: 6 waves of 64 x 32 (two-thirds of the 128 x 128 block's
   // staging and fragment reads per step for three-quarters of its MFMAs: more whole tiles where 128 x 128 leaves
@@ -1902,7 +1907,10 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
   constexpr int CA = (BM * BK / 8 + NTH - 1) / NTH, CB = BN * BK / 8 / NTH;
   constexpr int APAD = CA * NTH * 8;             // bf16 elements of a stage's A region
   constexpr int SLD = BN + 8;                    // epilogue staging row stride (floats)
-  constexpr int SMEM = NSTG * (APAD + BN * BK) > BM * SLD * 2 ? NSTG * (APAD + BN * BK) : BM * SLD * 2;  // + staging
+  // epilogue rows staged per pass: the whole 128-row tile at once; 64 rows at a time for 256-row tiles (the wave's 128
+  // accumulators stay live until its pass, so a pass's residual prefetch must stay small: 128-row passes spilled)
+  constexpr int EPR = BM == 128 ? 128 : 64, NPASS = BM / EPR;
+  constexpr int SMEM = NSTG * (APAD + BN * BK) > EPR * SLD * 2 ? NSTG * (APAD + BN * BK) : EPR * SLD * 2;  // + staging
   __shared__ __attribute__((aligned(16))) bf16 smem[SMEM];  // 96 KB at 3 stages of 128 x 128, the only LDS object
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wn = w - wm * WN, r = lane & 31, h = lane >> 5;  // wave tile 64 x WNC at (64 wm, WNC wn)
@@ -1928,10 +1936,10 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
                                                                        (int)(uint32_t)((size_t)N * K * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rs = attn_rsrc(ep.sk_ws);
   auto slab_off = [&](int slab, int i, int j, int q) {
-    return (uint32_t)(((((((size_t)slab * 8 + w) * 2 + i) * FJ + j) * 4 + q) * 64 + lane) * 16);
+    return (uint32_t)(((((((size_t)slab * 8 + w) * FI + i) * FJ + j) * 4 + q) * 64 + lane) * 16);
   };
   int* flag = reinterpret_cast<int*>(smem);
-  f32x16 acc[2][FJ];
+  f32x16 acc[FI][FJ];
 
   for (long it = it_begin; it < it_end;) {
     const int t = (int)(it / nk), k0 = (int)(it - (long)t * nk);
@@ -1970,7 +1978,7 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(Bs(buf) + (i * NTH + w * 64) * 8), 16, ob[i], off, 0, 0);
     };
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < FI; i++)
 #pragma unroll
       for (int j = 0; j < FJ; j++)
 #pragma unroll
@@ -1978,13 +1986,13 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
     auto ktile = [&](int buf) {
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ks++) {
-        bf16x8 af[2], bfr[FJ];
+        bf16x8 af[FI], bfr[FJ];
 #pragma unroll
-        for (int i = 0; i < 2; i++) af[i] = *reinterpret_cast<const bf16x8*>(As(buf) + sw(wm * 64 + i * 32 + r, ks * 2 + h));
+        for (int i = 0; i < FI; i++) af[i] = *reinterpret_cast<const bf16x8*>(As(buf) + sw(wm * (BM / 2) + i * 32 + r, ks * 2 + h));
 #pragma unroll
         for (int j = 0; j < FJ; j++) bfr[j] = *reinterpret_cast<const bf16x8*>(Bs(buf) + sw(wn * WNC + j * 32 + r, ks * 2 + h));
 #pragma unroll
-        for (int i = 0; i < 2; i++)
+        for (int i = 0; i < FI; i++)
 #pragma unroll
           for (int j = 0; j < FJ; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
@@ -2020,7 +2028,7 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
       // partial tile: fragments out, ticket; the last arriver sums the tile's segments in K order
       const int slab = 2 * b + (first_seg ? 0 : 1);
 #pragma unroll
-      for (int i = 0; i < 2; i++)
+      for (int i = 0; i < FI; i++)
 #pragma unroll
         for (int j = 0; j < FJ; j++)
 #pragma unroll
@@ -2043,7 +2051,7 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
       __syncthreads();  // the flag word is LDS the next segment overwrites
       if (!is_last) continue;
 #pragma unroll
-      for (int i = 0; i < 2; i++)
+      for (int i = 0; i < FI; i++)
 #pragma unroll
         for (int j = 0; j < FJ; j++) {
           f32x4 sum[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -2066,65 +2074,76 @@ __global__ __launch_bounds__(512) void gemm_mfma3_kernel(const bf16* __restrict_
     // the 96 KB at BN = 128), one barrier, then read back as 8-column chunks: one 16-B bf16 store (GELU, QKV) or two 16-B fp32
     // loads + stores (RESID) per chunk instead of 64 per-element accesses per lane.  The residual chunks and the
     // rows' cached lengths are loaded before the staging (clamped, unconditional: one round trip).
-    constexpr int NCH = BM * BN / 8 / NTH, CPR = BN / 8;  // chunks per thread (4 or 8), chunks per row
+    constexpr int NCH = EPR * BN / 8 / NTH, CPR = BN / 8;  // chunks per thread per pass (4 or 8), chunks per row
     float* stg = reinterpret_cast<float*>(smem);
     auto chunk_rc = [&](int c, int& lr, int& lc) { const int id = tid + c * NTH; lr = id / CPR; lc = (id % CPR) * 8; };
-    f32x4 rsd[NCH][2];
-    int cpast[NCH];
 #pragma unroll
-    for (int c = 0; c < NCH; c++) {
-      int lr, lc;
-      chunk_rc(c, lr, lc);
-      const int m = min(m0 + lr, M - 1), n = min(n0 + lc, N - 8);
-      if constexpr (EK == EPI_RESID) {
-        rsd[c][0] = *reinterpret_cast<const f32x4*>(ep.resid + (size_t)m * ep.ldo + n);
-        rsd[c][1] = *reinterpret_cast<const f32x4*>(ep.resid + (size_t)m * ep.ldo + n + 4);
-      }
-      if constexpr (EK == EPI_QKV) cpast[c] = ep.past_dev ? ep.past_dev[m / ep.seq] : ep.past;
-    }
+    for (int pass = 0; pass < NPASS; pass++) {
+      const int r0 = pass * EPR;  // the pass's first row of the tile (BM = 256: the rows of waves wm == pass)
+      f32x4 rsd[NCH][2];
+      int cpast[NCH];
+      auto epi_loads = [&]() {
 #pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-      for (int j = 0; j < FJ; j++)
-#pragma unroll
-        for (int e = 0; e < 16; e++)
-          stg[(wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * SLD + wn * WNC + j * 32 + r] = acc[i][j][e] * cscale[j] + bias[j];
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < NCH; c++) {
-      int lr, lc;
-      chunk_rc(c, lr, lc);
-      const int m = m0 + lr, n = n0 + lc;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + lr * SLD + lc);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + lr * SLD + lc + 4);
-      if (m >= M || n >= N) continue;
-      if constexpr (EK == EPI_RESID) {
-        float* o = ep.out_f32 + (size_t)m * ep.ldo + n;
-        *reinterpret_cast<f32x4*>(o) = v0 + rsd[c][0];
-        *reinterpret_cast<f32x4*>(o + 4) = v1 + rsd[c][1];
-      } else {
-        bf16x8 b8;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          b8[q] = from_f32<bf16>(EK == EPI_GELU ? gelu_bloom(v0[q]) : v0[q]);
-          b8[4 + q] = from_f32<bf16>(EK == EPI_GELU ? gelu_bloom(v1[q]) : v1[q]);
-        }
-        if constexpr (EK == EPI_GELU) {
-          *reinterpret_cast<bf16x8*>((bf16*)ep.out_act + (size_t)m * ep.ldo + n) = b8;
-        } else {
-          const int three = 3 * ep.head_dim;
-          const int head = n / three, rr = n - head * three, which = rr / ep.head_dim, d = rr - which * ep.head_dim;
-          bf16* dst;
-          if (which == 0) {
-            dst = (bf16*)ep.q_out + (size_t)m * ep.hidden + head * ep.head_dim + d;
-          } else {
-            const int bi = m / ep.seq, ti = m - bi * ep.seq;
-            dst = (bf16*)(which == 1 ? ep.k_cache : ep.v_cache) +
-                  (((size_t)(ep.slot + bi) * ep.n_head + head) * ep.max_ctx + cpast[c] + ti) * ep.head_dim + d;
+        for (int c = 0; c < NCH; c++) {
+          int lr, lc;
+          chunk_rc(c, lr, lc);
+          const int m = min(m0 + r0 + lr, M - 1), n = min(n0 + lc, N - 8);
+          if constexpr (EK == EPI_RESID) {
+            rsd[c][0] = *reinterpret_cast<const f32x4*>(ep.resid + (size_t)m * ep.ldo + n);
+            rsd[c][1] = *reinterpret_cast<const f32x4*>(ep.resid + (size_t)m * ep.ldo + n + 4);
           }
-          *reinterpret_cast<bf16x8*>(dst) = b8;
+          if constexpr (EK == EPI_QKV) cpast[c] = ep.past_dev ? ep.past_dev[m / ep.seq] : ep.past;
+        }
+      };
+      epi_loads();  // the residual / position loads go out before the staging (one round trip under it)
+#pragma unroll
+      for (int i = 0; i < FI; i++) {
+        if (NPASS > 1 && (wm * (BM / 2) + i * 32) / EPR != pass) continue;  // wave-uniform: fragment i is another pass's
+#pragma unroll
+        for (int j = 0; j < FJ; j++)
+#pragma unroll
+          for (int e = 0; e < 16; e++)
+            stg[(wm * (BM / 2) - r0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * SLD + wn * WNC + j * 32 + r] =
+                acc[i][j][e] * cscale[j] + bias[j];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < NCH; c++) {
+        int lr, lc;
+        chunk_rc(c, lr, lc);
+        const int m = m0 + r0 + lr, n = n0 + lc;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + lr * SLD + lc);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + lr * SLD + lc + 4);
+        if (m >= M || n >= N) continue;
+        if constexpr (EK == EPI_RESID) {
+          float* o = ep.out_f32 + (size_t)m * ep.ldo + n;
+          *reinterpret_cast<f32x4*>(o) = v0 + rsd[c][0];
+          *reinterpret_cast<f32x4*>(o + 4) = v1 + rsd[c][1];
+        } else {
+          bf16x8 b8;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            b8[q] = from_f32<bf16>(EK == EPI_GELU ? gelu_bloom(v0[q]) : v0[q]);
+            b8[4 + q] = from_f32<bf16>(EK == EPI_GELU ? gelu_bloom(v1[q]) : v1[q]);
+          }
+          if constexpr (EK == EPI_GELU) {
+            *reinterpret_cast<bf16x8*>((bf16*)ep.out_act + (size_t)m * ep.ldo + n) = b8;
+          } else {
+            const int three = 3 * ep.head_dim;
+            const int head = n / three, rr = n - head * three, which = rr / ep.head_dim, d = rr - which * ep.head_dim;
+            bf16* dst;
+            if (which == 0) {
+              dst = (bf16*)ep.q_out + (size_t)m * ep.hidden + head * ep.head_dim + d;
+            } else {
+              const int bi = m / ep.seq, ti = m - bi * ep.seq;
+              dst = (bf16*)(which == 1 ? ep.k_cache : ep.v_cache) +
+                    (((size_t)(ep.slot + bi) * ep.n_head + head) * ep.max_ctx + cpast[c] + ti) * ep.head_dim + d;
+            }
+            *reinterpret_cast<bf16x8*>(dst) = b8;
+          }
         }
       }
+      if (NPASS > 1 && pass + 1 < NPASS) __syncthreads();  // the staging rows are rewritten by the next pass
     }
     __syncthreads();  // the staging rows are overwritten next (the next segment's tiles)
   }
@@ -2191,14 +2210,33 @@ static int gemm3_pair_grid(int M, int N, int K, const Epi& ep) {
   return 0;
 }
 
-template <int NSTG = 3, bool XM = true, int BN = 128>
+template <int NSTG = 3, bool XM = true, int BN = 128, int BM = 128>
 static void gemm3_launch(const bf16* x, const bf16* w, int M, int N, int K, const Epi& ep, hipStream_t s, int G) {
   constexpr int NTH = BN == 256 ? 512 : 128 * (BN / 32);
   switch (ep.kind) {
-    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, NSTG, XM, BN><<<G, NTH, 0, s>>>(x, w, M, N, K, ep); break;
-    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, NSTG, XM, BN><<<G, NTH, 0, s>>>(x, w, M, N, K, ep); break;
-    default: gemm_mfma3_kernel<EPI_GELU, NSTG, XM, BN><<<G, NTH, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_QKV: gemm_mfma3_kernel<EPI_QKV, NSTG, XM, BN, BM><<<G, NTH, 0, s>>>(x, w, M, N, K, ep); break;
+    case EPI_RESID: gemm_mfma3_kernel<EPI_RESID, NSTG, XM, BN, BM><<<G, NTH, 0, s>>>(x, w, M, N, K, ep); break;
+    default: gemm_mfma3_kernel<EPI_GELU, NSTG, XM, BN, BM><<<G, NTH, 0, s>>>(x, w, M, N, K, ep); break;
   }
+}
+
+// 256 x 256 tiles (round 6): one whole tile per block (G = tiles: no partial tile, slab or ticket), two LDS stages,
+// for the big prefills (>= 16 K-steps, K <= 8192: bloom-7b1 fc2's K = 16384 ran 0.90-0.95x).  bloom-7b1 QKV at 4096
+// tokens 645 -> 397 us (639 -> 1040 TFLOP/s), fc1 605 -> 553, dense 164 -> 147; bloom-3b QKV 246 -> 185; every output
+// bit-identical to the 128 x 128 path (same K order).  0: not applicable.
+static int gemm3_big_grid(int M, int N, int K, const Epi& ep) {
+  // BS_GEMM_BIG=0 turns the 256 x 256 tiles off (tests compare the two paths bit for bit); read per call: prefill only
+  const char* off = getenv("BS_GEMM_BIG");
+  if (off && off[0] == '0') return 0;
+  if (K % 64 || N % 8 || ep.kind == EPI_ARGMAX || K / 64 < 16 || K > 8192) return 0;
+  if (ep.kind == EPI_QKV && ep.head_dim % 8) return 0;
+  if ((size_t)M * K * 2 >= (1ull << 32) || (size_t)N * K * 2 >= (1ull << 32)) return 0;
+  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  // >= 256 tiles that fill their last round of blocks to >= 70 % (288 tiles leave 224 CUs idle in the second round:
+  // bloom-1b1 QKV at 4096 tokens 0.96x; 256 / 384 / 480 tiles 1.12-1.33x, profiles/r06_gemm_256x256_ab.txt)
+  const long rounds = (tiles + 255) / 256;
+  if (tiles < 256 || tiles * 10 < rounds * 256 * 7 || tiles > (1L << 20)) return 0;
+  return (int)tiles;
 }
 
 // 128 x 96 tiles (6 waves), whole tiles, one per block: where 128 x 128 tiles leave CUs idle (< 200 tiles) and the
@@ -2463,7 +2501,9 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
   if ((K % 64) == 0) {
     // 128x128 when it still gives every CU a block (>= 240 blocks), else 64x64, else 64x32
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-    if (const int gw = gemm3_wide_grid(M, N, K, ep)) {
+    if (const int gb = gemm3_big_grid(M, N, K, ep)) {
+      gemm3_launch<2, true, 256, 256>(x, w, M, N, K, ep, s, gb);
+    } else if (const int gw = gemm3_wide_grid(M, N, K, ep)) {
       gemm3_launch<3, true, 256>(x, w, M, N, K, ep, s, gw);
     } else if (const int gp = gemm3_pair_grid(M, N, K, ep)) {
       gemm3_launch<2>(x, w, M, N, K, ep, s, gp);

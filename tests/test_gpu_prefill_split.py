@@ -86,3 +86,28 @@ def test_prefill_two_query_groups_many_rows(h):
     print(f"h={h}: two-query-group prefill {B}x{S} max-abs {err:.3e}")
     gs.close()
     os_.close()
+
+
+def test_prefill_256_tiles_bitwise_equal_to_128_tiles():
+    """Big prefills (>= 512 whole 256 x 256 tiles, K <= 8192) run gemm_mfma3 on 256 x 256 tiles (round 6); every output
+    element sums K in the same order as the 128 x 128 path, so a bloom-7b1-width layer over 16 rows x 512 tokens (QKV,
+    dense, fc1 on 256 x 256 tiles: 1536 / 512 / 2048 tiles; fc2, K = 16384, stays on 128 x 128) gives the same bits
+    with the big tiles switched off (BS_GEMM_BIG=0): hidden states and the K/V rows written by the QKV epilogue."""
+    import os
+    h, nh, B, S = 4096, 32, 16, 512
+    x = (0.5 * np.random.default_rng(21).standard_normal((B, S, h))).astype(np.float32)
+    out = {}
+    for big in ("1", "0"):
+        os.environ["BS_GEMM_BIG"] = big
+        try:
+            gs = Stage(h, nh, 1, 512, 0, 1, dtype="bf16", max_batch=B, max_ctx=S, max_tokens=B * S, seed=7,
+                       is_first=False, is_last=False)
+            y = gs.forward_host(x, B, S, past_len=0)
+            kv = gs.read_kv(0, B - 1, 0, S)
+            gs.close()
+        finally:
+            os.environ.pop("BS_GEMM_BIG", None)
+        out[big] = (y, kv)
+    assert np.isfinite(out["1"][0]).all()
+    assert np.array_equal(out["1"][0].view(np.uint32), out["0"][0].view(np.uint32))
+    assert np.array_equal(out["1"][1].view(np.uint32), out["0"][1].view(np.uint32))

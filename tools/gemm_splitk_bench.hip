@@ -4,10 +4,13 @@
 // same products summed in another order: max relative difference printed); gemm_mfma3 (128x128 tiles on
 // v_mfma_f32_32x32x16_bf16, stream-K) at the dispatch's grid with and without the XCD-aware placement (XM), and at
 // grids of 192..512 blocks.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/gemm_splitk_bench.hip -o tools/gemm_splitk_bench
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/gemm_splitk_bench.hip
+//        distributed_inference_demo_amd/csrc/attn_prefill.hip -o tools/gemm_splitk_bench
 #include "../distributed_inference_demo_amd/csrc/kernels.hip"
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
+#include <cstdlib>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
@@ -29,9 +32,16 @@ int main() {
       {"1b1 fc1 4k", 4096, 6144, 1536}, {"1b1 qkv 4k", 4096, 4608, 1536},
       // bloom-1b1 at 1024 / 2048 tokens (288..1536 tiles: where whole-tile grids of 384 / 512 blocks might apply)
       {"1b1 qkv 1k", 1024, 4608, 1536}, {"1b1 fc1 1k", 1024, 6144, 1536}, {"1b1 fc2 1k", 1024, 1536, 6144},
-      {"1b1 qkv 2k", 2048, 4608, 1536}, {"1b1 fc1 2k", 2048, 6144, 1536}, {"1b1 fc2 2k", 2048, 1536, 6144}};
+      {"1b1 qkv 2k", 2048, 4608, 1536}, {"1b1 fc1 2k", 2048, 6144, 1536}, {"1b1 fc2 2k", 2048, 1536, 6144},
+      // round 6: configs[4]'s prefills (16 rows x 256 .. 1024 tokens per micro-batch at N = 1), 256 x 256 tiles
+      {"7b1 qkv 4k", 4096, 12288, 4096}, {"7b1 dense 4k", 4096, 4096, 4096}, {"7b1 fc1 4k", 4096, 16384, 4096},
+      {"7b1 fc2 4k", 4096, 4096, 16384}, {"7b1 qkv 16k", 16384, 12288, 4096}, {"7b1 fc1 16k", 16384, 16384, 4096},
+      {"7b1 fc2 16k", 16384, 4096, 16384}, {"7b1 dense 16k", 16384, 4096, 4096}, {"7b1 fc2 8k", 8192, 4096, 16384},
+      {"7b1 qkv 3840", 3840, 12288, 4096}, {"7b1 dense 3840", 3840, 4096, 4096}, {"3b qkv 4k", 4096, 7680, 2560},
+      {"3b fc1 4k", 4096, 10240, 2560}, {"3b fc2 4k", 4096, 2560, 10240}};
+  const char* only = getenv("GSB_ONLY");  // substring filter on the shape names
   bf16 *X, *W, *bias; float *out, *ref, *resid, *ws; unsigned* tick;
-  const size_t MMAX = 4096;
+  const size_t MMAX = 16384;
   CK(hipMalloc(&X, MMAX * 16384 * 2)); CK(hipMalloc(&W, (size_t)16384 * 16384 * 2));
   CK(hipMalloc(&bias, 65536 * 2)); CK(hipMalloc(&out, MMAX * 16384 * 4)); CK(hipMalloc(&ref, MMAX * 16384 * 4));
   CK(hipMalloc(&resid, MMAX * 16384 * 4)); CK(hipMemset(resid, 0, MMAX * 16384 * 4));
@@ -42,6 +52,7 @@ int main() {
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (auto& sh : shapes) {
+    if (only && !strstr(sh.name, only)) continue;
     const int M = sh.M, N = sh.N, K = sh.K;
     Epi ep{};
     ep.kind = EPI_RESID; ep.bias = bias; ep.out_f32 = out; ep.resid = resid; ep.ldo = N;
@@ -84,6 +95,19 @@ int main() {
       line(nm, us);
       if (md > 1e-4) printf("           MISMATCH max |diff| %.3g\n", md);
     };
+    // every shape with >= 256 whole 256 x 256 tiles, whether or not the library's dispatch takes them (threshold sweep)
+    const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+    if (const int gb = (K % 64 == 0 && t256 >= 256) ? (int)t256 : 0) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "m32 256x256 G=%d", gb);
+      const float us = timeit([&] { gemm3_launch<2, true, 256, 256>(X, W, M, N, K, ep, 0, gb); });
+      CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (size_t i = 0; i < ho.size(); i++) md = std::max(md, (double)fabsf(ho[i] - hr[i]));
+      line(nm, us);
+      printf("           max |diff| vs 64x32 %.3g%s\n", md, md > 1e-3 ? "  MISMATCH" : "");
+    }
+    if (M > 4096) continue;  // the big shapes: the library and the 256 x 256 tiles only
     for (int ks : {1, 4})
       variant("64x64 r4", 64, 64, ks, [&] { gemm2_launch<64, 64, 4>(X, W, M, N, K, ep, 0, ks); });
     if (const int G = gemm3_grid(M, N, K, ep)) {
