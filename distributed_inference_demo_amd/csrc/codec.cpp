@@ -122,3 +122,19 @@ extern "C" int bs_deserialize_int(const uint8_t* bytes, uint64_t len, int32_t* v
   std::memcpy(value, bytes, 4);
   return BS_OK;
 }
+
+extern "C" int bs_binary_classify(const void* bytes, uint64_t len, int32_t* cls) {
+  // binaryClassify (native-lib.cpp:128-160): first tensor of the vector = logits; binary_classify
+  // (inference.cpp:57-69) scans the first two floats with a strict >, so the first maximum wins.
+  if (!cls) return BS_ERR_INVALID;
+  bs_tensor_view v;
+  int32_t n = 0;
+  const int rc = bs_codec_deserialize(bytes, len, &v, 1, &n);
+  if (rc != BS_OK) return rc;
+  uint64_t cnt = 0;
+  if (n < 1 || v.dtype != BS_DT_FLOAT || !elem_count(v, &cnt) || cnt < 2) return BS_ERR_INVALID;
+  float l[2];
+  std::memcpy(l, v.data, sizeof l);  // the view may be unaligned inside the wire buffer
+  *cls = l[1] > l[0] ? 1 : 0;
+  return BS_OK;
+}

@@ -126,6 +126,10 @@ void launch_linear_parts(const AttnParts& p, const void* W, int M, int N, int K,
 void launch_argmax_finalize(const unsigned long long* keys, int M, int ntiles, const unsigned long long* keys_in,
                             unsigned long long* keys_out, int* tokens, hipStream_t s, int* past_adv = nullptr,
                             int seq = 0);
+// Sequence-classification head: xn (T) [M][K] . score (T) [n_labels][K] -> logits fp32 [M][n_labels] (optional),
+// cls[m] = first maximal label (inference.cpp:57-69); past_adv[m] += seq (optional).  n_labels <= 64, K % 8 == 0.
+void launch_classify(int is_bf16, const void* xn, const void* score, int M, int n_labels, int K, float* logits,
+                     int* cls, int* past_adv, int seq, hipStream_t s);
 // past_dev[0..n) = values[0..n) (host), stream ordered, by kernel arguments (graph-capturable).
 // Seeded top-k sampling (include/bloomstage.h bs_set_sampling; decoding.cpp:24-66) of M rows from the
 // per-16-column tile keys (key_hi_index = 1) and the logits they came from ([M][ldl], column = vocab index).

@@ -2910,6 +2910,54 @@ void launch_argmax_finalize(const unsigned long long* keys, int M, int ntiles, c
 }
 
 // ------------------------------------------------------------------------------------
+// Sequence-classification head (BS_FLAG_CLASSIFIER): logits[m][c] = xn[m] . score[c] (fp32 accumulation; no bias,
+// BloomForSequenceClassification.score), class[m] = the first c of the largest logit (binary_classify,
+// inference.cpp:57-69: a strict > scan).  n_labels <= 64 rows of K weights are a few KB: one 256-thread block per
+// row, wave w takes labels w, w + 4, ...; each lane streams 16-B vectors of the row and the label.  The step's last
+// kernel: advances past_adv[m] by seq like argmax_finalize.
+template <typename T>
+__global__ __launch_bounds__(256) void classify_kernel(const T* __restrict__ xn, const T* __restrict__ w, int n_labels,
+                                                       int K, float* __restrict__ logits, int* __restrict__ cls,
+                                                       int* past_adv, int seq) {
+  __shared__ float lg[64];
+  const int m = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const T* x = xn + (size_t)m * K;
+  for (int c = wave; c < n_labels; c += 4) {
+    const T* wr = w + (size_t)c * K;
+    float acc = 0.f;
+    for (int k = lane * 8; k < K; k += 64 * 8) {
+      float xv[8], wv[8];
+      load8(x + k, xv);
+      load8(wr + k, wv);
+#pragma unroll
+      for (int j = 0; j < 8; j++) acc = fmaf(xv[j], wv[j], acc);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) lg[c] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int best = 0;
+    for (int c = 1; c < n_labels; c++)
+      if (lg[c] > lg[best]) best = c;
+    cls[m] = best;
+    if (past_adv) past_adv[m] += seq;
+  }
+  if (logits)
+    for (int c = threadIdx.x; c < n_labels; c += 256) logits[(size_t)m * n_labels + c] = lg[c];
+}
+
+void launch_classify(int is_bf16, const void* xn, const void* score, int M, int n_labels, int K, float* logits,
+                     int* cls, int* past_adv, int seq, hipStream_t s) {
+  if (is_bf16)
+    classify_kernel<bf16><<<M, 256, 0, s>>>((const bf16*)xn, (const bf16*)score, n_labels, K, logits, cls, past_adv, seq);
+  else
+    classify_kernel<float><<<M, 256, 0, s>>>((const float*)xn, (const float*)score, n_labels, K, logits, cls, past_adv,
+                                             seq);
+}
+
+// ------------------------------------------------------------------------------------
 // Seeded top-k sampling, restating decoding::StaticDecoding (decoding.cpp:24-66) on the tile keys of
 // the lm_head epilogue (key = order(logit) << 32 | vocab index: std::greater on (value, index)).
 // One 1024-thread block per row.  (1) The top-k TILES by their max key: every element of the row's

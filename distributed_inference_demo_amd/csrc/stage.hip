@@ -54,7 +54,7 @@ namespace {
 
 enum { T_LN1_G, T_LN1_B, T_QKV_W, T_QKV_B, T_DENSE_W, T_DENSE_B, T_LN2_G, T_LN2_B, T_FC1_W, T_FC1_B,
        T_FC2_W, T_FC2_B, T_NLAYER };
-enum { M_WEMB = 0, M_EMB_G = 1, M_EMB_B = 2, M_LNF_G = 3, M_LNF_B = 4 };
+enum { M_WEMB = 0, M_EMB_G = 1, M_EMB_B = 2, M_LNF_G = 3, M_LNF_B = 4, M_SCORE = 5 };
 
 struct Layer {
   void* t[T_NLAYER];
@@ -115,6 +115,8 @@ struct bs_stage {
   void* lnf_b = nullptr;
   void* hw = nullptr;     // head slice rows [hv0, hv1) of the tied lm_head (may point into wemb)
   int hv0 = 0, hv1 = 0;
+  void* score = nullptr;  // BS_FLAG_CLASSIFIER: score [n_labels][hidden] (the head instead of the lm_head)
+  int n_labels = 0;
   std::vector<Layer> layers;
   char* kv = nullptr;  // [L][2][max_batch][heads][max_ctx][hd]
   size_t kvbytes = 0;
@@ -215,7 +217,12 @@ static int validate(const bs_stage_desc* d, bool from_file = false) {
     return fail(BS_ERR_INVALID, "head vocab slice must be a 16-aligned sub-range of [0, vocab)");
   if (!from_file && d->weight_source != BS_WEIGHTS_SYNTHETIC && d->weight_source != BS_WEIGHTS_HOST)
     return fail(BS_ERR_INVALID, "unknown weight_source");
-  if (d->flags & ~BS_FLAG_INT8_WEIGHTS) return fail(BS_ERR_INVALID, "unknown desc flags");
+  if (d->flags & ~(BS_FLAG_INT8_WEIGHTS | BS_FLAG_CLASSIFIER)) return fail(BS_ERR_INVALID, "unknown desc flags");
+  if (d->flags & BS_FLAG_CLASSIFIER) {
+    if (!d->is_last) return fail(BS_ERR_INVALID, "BS_FLAG_CLASSIFIER needs the last stage");
+    if (d->n_labels < 1 || d->n_labels > 64) return fail(BS_ERR_INVALID, "n_labels must be in [1, 64]");
+    if (d->head_vocab_end > d->head_vocab_begin) return fail(BS_ERR_INVALID, "a classifier stage takes no head slice");
+  }
   if ((d->flags & BS_FLAG_INT8_WEIGHTS) && d->dtype != BS_DT_BFLOAT16)
     return fail(BS_ERR_UNSUPPORTED, "BS_FLAG_INT8_WEIGHTS needs dtype BFLOAT16");
   return BS_OK;
@@ -225,10 +232,12 @@ extern "C" uint64_t bs_stage_weight_count(const bs_stage_desc* d) {
   if (validate(d) != BS_OK) return 0;
   const uint64_t h = (uint64_t)d->hidden;
   uint64_t n = 0;
-  if (d->is_first || d->is_last) n += (uint64_t)d->vocab * h;
+  const bool cls = (d->flags & BS_FLAG_CLASSIFIER) != 0;
+  if (d->is_first || (d->is_last && !cls)) n += (uint64_t)d->vocab * h;
   if (d->is_first) n += 2 * h;
   n += (uint64_t)(d->layer_end - d->layer_begin) * (12 * h * h + 13 * h);
   if (d->is_last) n += 2 * h;
+  if (cls) n += (uint64_t)d->n_labels * h;
   const bool slice = d->head_vocab_end > d->head_vocab_begin;
   if (slice && !d->is_first && !d->is_last) n += (uint64_t)(d->head_vocab_end - d->head_vocab_begin) * h;
   if (slice && !d->is_last) n += 2 * h;
@@ -282,7 +291,8 @@ struct FileEntry {
 static std::vector<FileEntry> file_entries(const bs_stage_desc* d) {
   const int64_t h = d->hidden, V = d->vocab;
   std::vector<FileEntry> e;
-  if (d->is_first || d->is_last) e.push_back({"word_embeddings.weight", 0, {V, h}});
+  const bool cls = (d->flags & BS_FLAG_CLASSIFIER) != 0;
+  if (d->is_first || (d->is_last && !cls)) e.push_back({"word_embeddings.weight", 0, {V, h}});
   if (d->is_first) {
     e.push_back({"word_embeddings_layernorm.weight", 0, {h}});
     e.push_back({"word_embeddings_layernorm.bias", 0, {h}});
@@ -297,6 +307,7 @@ static std::vector<FileEntry> file_entries(const bs_stage_desc* d) {
   for (int l = d->layer_begin; l < d->layer_end; l++)
     for (int t = 0; t < T_NLAYER; t++) e.push_back({"h." + std::to_string(l) + "." + tn[t], 0, ts[t]});
   if (d->is_last) { e.push_back({"ln_f.weight", 0, {h}}); e.push_back({"ln_f.bias", 0, {h}}); }
+  if (cls) e.push_back({"score.weight", 0, {(int64_t)d->n_labels, h}});  // BloomForSequenceClassification.score
   const bool slice = d->head_vocab_end > d->head_vocab_begin;
   if (slice && !d->is_first && !d->is_last) e.push_back({"word_embeddings.weight", (uint64_t)d->head_vocab_begin * h, {V, h}});
   if (slice && !d->is_last) { e.push_back({"ln_f.weight", 0, {h}}); e.push_back({"ln_f.bias", 0, {h}}); }
@@ -394,6 +405,7 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   s->bf16 = desc->dtype == BS_DT_BFLOAT16;
   s->q8 = (desc->flags & BS_FLAG_INT8_WEIGHTS) != 0;
   s->esz = s->bf16 ? 2 : 4;
+  s->n_labels = (desc->flags & BS_FLAG_CLASSIFIER) ? desc->n_labels : 0;
   s->hd = desc->hidden / desc->n_head;
   s->L = desc->layer_end - desc->layer_begin;
   const size_t h = desc->hidden, V = desc->vocab, T = s->d.max_tokens;
@@ -408,7 +420,8 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   std::vector<size_t> offs;
   auto add = [&](size_t n) { offs.push_back(off); off = align_up(off + n * s->esz, 256); };
   auto addb = [&](size_t bytes) { offs.push_back(off); off = align_up(off + bytes, 256); };
-  if (desc->is_first || desc->is_last) add(V * h);
+  const bool own_emb = desc->is_first || (desc->is_last && !s->n_labels);
+  if (own_emb) add(V * h);
   if (desc->is_first) { add(h); add(h); }
   size_t lsz[T_NLAYER];
   layer_sizes(h, lsz);
@@ -422,6 +435,7 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
       }
     }
   if (desc->is_last) { add(h); add(h); }
+  if (s->n_labels) add((size_t)s->n_labels * h);
   const bool slice = desc->head_vocab_end > desc->head_vocab_begin;
   s->hv0 = desc->head_vocab_begin;
   s->hv1 = desc->head_vocab_end;
@@ -432,7 +446,7 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   if (hipMalloc(&s->wbase, s->wbytes ? s->wbytes : 256) != hipSuccess)
     return cleanup(fail(BS_ERR_OOM, "weight allocation failed (" + std::to_string(s->wbytes) + " B)"));
   size_t oi = 0;
-  if (desc->is_first || desc->is_last) s->wemb = s->wbase + offs[oi++];
+  if (own_emb) s->wemb = s->wbase + offs[oi++];
   if (desc->is_first) { s->emb_g = s->wbase + offs[oi++]; s->emb_b = s->wbase + offs[oi++]; }
   s->layers.resize(s->L);
   for (int l = 0; l < s->L; l++)
@@ -441,11 +455,12 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
       s->layers[l].sc[t] = (s->q8 && is_matrix(t)) ? (float*)(s->wbase + offs[oi++]) : nullptr;
     }
   if (desc->is_last) { s->lnf_g = s->wbase + offs[oi++]; s->lnf_b = s->wbase + offs[oi++]; }
+  if (s->n_labels) s->score = s->wbase + offs[oi++];
   if (slice) {
     if (s->wemb) s->hw = (char*)s->wemb + (size_t)s->hv0 * h * s->esz;
     else s->hw = s->wbase + offs[oi++];
     if (!desc->is_last) { s->lnf_g = s->wbase + offs[oi++]; s->lnf_b = s->wbase + offs[oi++]; }
-  } else if (desc->is_last) {
+  } else if (desc->is_last && !s->n_labels) {
     s->hw = s->wemb; s->hv0 = 0; s->hv1 = desc->vocab;  // the last stage's full head
   }
   if (s->wemb) s->order.push_back({s->wemb, V * h});
@@ -453,6 +468,7 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
   for (int l = 0; l < s->L; l++)
     for (int t = 0; t < T_NLAYER; t++) s->order.push_back({s->layers[l].t[t], lsz[t]});
   if (desc->is_last) { s->order.push_back({s->lnf_g, h}); s->order.push_back({s->lnf_b, h}); }
+  if (s->score) s->order.push_back({s->score, (size_t)s->n_labels * h});
   if (slice && !desc->is_first && !desc->is_last) s->order.push_back({s->hw, hrows * h});
   if (slice && !desc->is_last) { s->order.push_back({s->lnf_g, h}); s->order.push_back({s->lnf_b, h}); }
   s->order_q8.assign(s->order.size(), {nullptr, 0});
@@ -548,6 +564,7 @@ static int init_stage(const bs_stage_desc* desc, bs_stage** out, const st::Check
       launch_gen_fill(s->hw, s->bf16, hrows * h, tensor_key(seed, -1, M_WEMB), 0, s->own, (uint64_t)s->hv0 * h);
     if (s->lnf_g) launch_gen_fill(s->lnf_g, s->bf16, h, tensor_key(seed, -1, M_LNF_G), 2, s->own);
     if (s->lnf_b) launch_gen_fill(s->lnf_b, s->bf16, h, tensor_key(seed, -1, M_LNF_B), 3, s->own);
+    if (s->score) launch_gen_fill(s->score, s->bf16, (size_t)s->n_labels * h, tensor_key(seed, -1, M_SCORE), 0, s->own);
   } else {
     const uint64_t need = bs_stage_weight_count(desc);
     if (!desc->host_weights || desc->host_weight_count != need)
@@ -1138,7 +1155,23 @@ static int enqueue_forward(bs_stage* s, const bs_step* step, const void* in, voi
   }
 
   // ---- output
-  if (d.is_last) {
+  if (d.is_last && s->n_labels) {
+    // sequence-classification tail (run_inference_with_binary_classification, inference.cpp:220-270): ln_f on each
+    // row's last position, score, first maximal class; the class kernel is the step's last (advances past_dev)
+    float* dev_logits = want_logits && !host_io ? logits : nullptr;
+    if (want_logits && host_io) {
+      int rc = logits_staging(s, (size_t)B * s->n_labels * 4, st, &dev_logits);
+      if (rc != BS_OK) return rc;
+    }
+    launch_layernorm(s->bf16, cur, nullptr, S, S - 1, s->lnf_g, s->lnf_b, s->xn, 0, B, h, d.ln_eps, st);
+    int* cls_out = host_io ? s->tok : (int*)out;
+    launch_classify(s->bf16, s->xn, s->score, B, s->n_labels, h, dev_logits, cls_out, s->past_dev, S, st);
+    if (host_io) {
+      HIP_TRY(hipMemcpyAsync(out, s->tok, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+      if (dev_logits)
+        HIP_TRY(hipMemcpyAsync(logits, dev_logits, (size_t)B * s->n_labels * 4, hipMemcpyDeviceToHost, st));
+    }
+  } else if (d.is_last) {
     // ln_f on each row's last position, tied lm_head, token pick (greedy argmax or top-k sample)
     const bool sample = s->top_k > 1;
     Epi e{};
@@ -1204,7 +1237,8 @@ extern "C" int bs_head_slice(bs_stage* s, const void* xn, int32_t B, const uint6
 extern "C" int bs_set_sampling(bs_stage* s, int32_t top_k, float temperature, uint64_t seed) {
   if (!s) return fail(BS_ERR_INVALID, "stage is NULL");
   if (top_k > 16) return fail(BS_ERR_UNSUPPORTED, "top_k must be <= 16");
-  if (top_k > 1 && !s->d.is_last) return fail(BS_ERR_UNSUPPORTED, "sampling needs the last stage (whole lm_head)");
+  if (top_k > 1 && (!s->d.is_last || s->n_labels))
+    return fail(BS_ERR_UNSUPPORTED, "sampling needs the last stage of a generation model (whole lm_head)");
   if (top_k > 1 && !(temperature > 0.f)) return fail(BS_ERR_INVALID, "temperature must be positive");
   HIP_TRY(hipSetDevice(s->d.device));
   if (top_k > 1 && !s->sample_logits) {

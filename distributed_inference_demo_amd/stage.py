@@ -7,11 +7,13 @@ Reference interface (Java side `Communication.java:1153-1182`, C++ side `native-
     Object[] runInferenceMasterResidual(long, int[] ids, int[] seq, int[][] res)   :942-1034
     Object[] runInferenceWorkerResidual(long, byte[] seq, ArrayList<byte[]> res, int[], int[][])  :1036-1194
     byte[] runInferenceWorkerResidualLastGeneration(long, byte[] seq, ArrayList<byte[]> res, int k, float temp)  :1368-1443
+    byte[] runInferenceWorkerResidualLastClassification(long, byte[] seq, ArrayList<byte[]> res)  :1305-1366
+    int    binaryClassify(byte[])                                            :128-160
     int    deserializeInt(byte[])                                            :1445-1471
 
 `create_session`, `release_session`, `run_inference_master_residual`,
-`run_inference_worker_residual`, `run_inference_worker_residual_last_generation` and
-`deserialize_int` below keep those names, argument meanings and wire formats (activations as
+`run_inference_worker_residual`, `run_inference_worker_residual_last_generation`,
+`run_inference_worker_residual_last_classification`, `binary_classify` and `deserialize_int` below keep those names, argument meanings and wire formats (activations as
 the utils.cpp tensor-vector bytes, the tail's token as 4 little-endian bytes) so the
 reference's driver loop ports over unchanged.  They run the stage with host I/O.  The fast
 path is `Stage.forward()` on device buffers (what the RCCL pipeline uses).
@@ -38,6 +40,7 @@ BS_WEIGHTS_HOST = 1
 BS_STEP_HOST_IO = 1
 BS_STEP_LOGITS = 2
 BS_FLAG_INT8_WEIGHTS = 1  # bs_stage_desc.flags: weight-only int8 block matrices
+BS_FLAG_CLASSIFIER = 2    # bs_stage_desc.flags: sequence-classification tail (score head, class ids out)
 
 DTYPES = {
     1: np.float32, 2: np.uint8, 3: np.int8, 4: np.uint16, 5: np.int16, 6: np.int32, 7: np.int64,
@@ -61,7 +64,7 @@ class StageDesc(ctypes.Structure):
         ("weight_source", ctypes.c_int32), ("seed", ctypes.c_uint64),
         ("host_weights", ctypes.c_void_p), ("host_weight_count", ctypes.c_uint64),
         ("head_vocab_begin", ctypes.c_int32), ("head_vocab_end", ctypes.c_int32),
-        ("flags", ctypes.c_int32),
+        ("flags", ctypes.c_int32), ("n_labels", ctypes.c_int32),
     ]
 
 
@@ -82,7 +85,7 @@ EXPORTS = [
     "bs_codec_serialize", "bs_codec_deserialize", "bs_dtype_size", "bs_serialize_int", "bs_deserialize_int",
     "bs_prompt_ids", "bs_read_weights", "bs_head_norm", "bs_head_slice", "bs_stream_delay", "bs_set_sampling",
     "bs_build_id", "bs_hbm_probe", "bs_mfma_probe", "bs_init_stage_file", "bs_weights_file_probe",
-    "bs_set_graphs",
+    "bs_set_graphs", "bs_binary_classify",
 ]
 
 _LIB = None
@@ -129,6 +132,7 @@ def lib():
         L.bs_serialize_int.argtypes = [i32, ctypes.c_char_p]
         L.bs_serialize_int.restype = None
         L.bs_deserialize_int.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(i32)]
+        L.bs_binary_classify.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(i32)]
         L.bs_prompt_ids.argtypes = [ctypes.c_uint64, i32, i32, vp]
         L.bs_read_weights.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, vp]
         L.bs_head_norm.argtypes = [vp, vp, i32, i32, vp, vp]
@@ -173,9 +177,11 @@ class Stage:
 
     def __init__(self, hidden, n_head, n_layer, vocab, layer_begin, layer_end, *, dtype="bf16", device=0,
                  max_batch=1, max_ctx=2048, max_tokens=0, seed=0, eps=1e-5, host_weights=None,
-                 is_first=None, is_last=None, head_slice=None, int8_weights=False, weights_file=None):
+                 is_first=None, is_last=None, head_slice=None, int8_weights=False, weights_file=None, n_labels=0):
         """weights_file: a safetensors checkpoint (or its sharded *.index.json) of HF BLOOM tensors;
-        the stage maps it and loads only its own layer range (bs_init_stage_file)."""
+        the stage maps it and loads only its own layer range (bs_init_stage_file).
+        n_labels > 0: a sequence-classification tail (BS_FLAG_CLASSIFIER, last stage): forwards return class ids
+        and logits [batch][n_labels] instead of tokens and vocabulary logits."""
         if weights_file is not None and host_weights is not None:
             raise ValueError("pass host_weights or weights_file, not both")
         d = StageDesc()
@@ -187,6 +193,9 @@ class Stage:
         d.device, d.max_batch, d.max_ctx, d.max_tokens = device, max_batch, max_ctx, max_tokens
         d.seed = seed
         d.flags = BS_FLAG_INT8_WEIGHTS if int8_weights else 0  # bloom*-int8 variants (server.py:796-799)
+        if n_labels:
+            d.flags |= BS_FLAG_CLASSIFIER
+            d.n_labels = n_labels
         if head_slice is not None:
             d.head_vocab_begin, d.head_vocab_end = head_slice
         self._weights_ref = None
@@ -200,6 +209,8 @@ class Stage:
             d.weight_source = BS_WEIGHTS_SYNTHETIC
         self.desc = d
         self.hidden, self.vocab = hidden, vocab
+        self.n_labels = n_labels
+        self.n_out = n_labels if n_labels else vocab  # logits per row of the last stage
         self.is_first, self.is_last = bool(d.is_first), bool(d.is_last)
         self.max_batch, self.max_ctx = max_batch, max_ctx
         h = ctypes.c_void_p()
@@ -275,7 +286,7 @@ class Stage:
         else:
             x = np.ascontiguousarray(x, dtype=np.float32).reshape(batch, seq, self.hidden)
         out = np.empty(batch, np.int32) if self.is_last else np.empty((batch, seq, self.hidden), np.float32)
-        logits = np.empty((batch, self.vocab), np.float32) if want_logits else None
+        logits = np.empty((batch, self.n_out), np.float32) if want_logits else None
         flags = BS_STEP_HOST_IO | (BS_STEP_LOGITS if want_logits else 0)
         st, pasts = self._step(batch, seq, slot, past_len, flags)
         _check(lib().bs_forward(self._h, ctypes.byref(st), x.ctypes.data, out.ctypes.data,
@@ -487,6 +498,25 @@ def run_inference_worker_residual_last_generation(stage: Stage, seq_bytes: bytes
         stage._pick = pick
     tok = stage.forward_host(x, 1, S)
     return serialize_int(int(tok[0]))
+
+
+def run_inference_worker_residual_last_classification(stage: Stage, seq_bytes: bytes, residuals=()) -> bytes:
+    """runInferenceWorkerResidualLastClassification (native-lib.cpp:1305-1366): classifier tail stage
+    (Stage(..., n_labels=...)), returns the class of the sample -- the first index of the largest score logit,
+    inference::binary_classify (inference.cpp:57-69) -- as 4 little-endian bytes (utils::SerializeInt)."""
+    if not stage.n_labels:
+        raise BloomStageError("classification entry called on a stage without a classifier head")
+    x = deserialize_tensors(seq_bytes)[0].astype(np.float32, copy=False)
+    cls = stage.forward_host(x, 1, x.shape[-2])
+    return serialize_int(int(cls[0]))
+
+
+def binary_classify(data: bytes) -> int:
+    """binaryClassify (native-lib.cpp:128-160): the first tensor of a wire buffer holds logits; the class is the
+    first index of the larger of its first two floats (bs_binary_classify)."""
+    v = ctypes.c_int32()
+    _check(lib().bs_binary_classify(bytes(data), len(data), ctypes.byref(v)))
+    return v.value
 
 
 def unpack_int_be(data: bytes) -> int:

@@ -14,6 +14,11 @@
  *   bs_reset_kv        <- (none: the reference has no KV cache; new sample == new slot)
  *   bs_last_error      <- (none: the reference throws C++ exceptions across JNI,
  *                         native-lib.cpp:986-988; here errors are status codes + this string)
+ *   bs_forward on a BS_FLAG_CLASSIFIER stage
+ *                      <- runInferenceWorkerResidualLastClassification (native-lib.cpp:1305-1366)
+ *                         -> inference::run_inference_with_binary_classification (inference.cpp:220-270)
+ *   bs_binary_classify <- Java_..._binaryClassify (native-lib.cpp:128-160) -> inference::binary_classify
+ *                         (inference.cpp:57-69)
  *   bs_codec_*         <- utils::SerializeTensorVectorToBytes / DeserializeTensorVectorFromBytes
  *                         (utils.cpp:124-264 / :266-368), byte-exact wire format
  *   bs_serialize_int / bs_deserialize_int
@@ -33,7 +38,7 @@
 extern "C" {
 #endif
 
-#define BS_ABI_VERSION 2
+#define BS_ABI_VERSION 3
 
 typedef enum {
   BS_OK = 0,
@@ -63,6 +68,16 @@ typedef enum {
  * LayerNorms, biases and the tied lm_head stay bf16; activations stay bf16/fp32 (weight-only).
  * bs_read_weights returns Q * scale for the quantized matrices. */
 #define BS_FLAG_INT8_WEIGHTS 1
+/* desc->flags.  BS_FLAG_CLASSIFIER (last stage): the tail of a BLOOM sequence classifier -- the reference's
+ * classification task (task_type "classification", Communication.java:532, :596) whose tail sub-model ends in
+ * logits that inference::binary_classify reduces to a class (inference.cpp:57-69, :220-270).  The head is HF
+ * BloomForSequenceClassification's: ln_f on each row's last position (the pooled token of an unpadded row), then
+ * score = Linear(hidden, n_labels, bias=False) -- checkpoint tensor "score.weight" [n_labels][hidden], canonical
+ * order after ln_f -- instead of the tied lm_head.  bs_forward's out is an int32 class per row, the FIRST index
+ * of the largest logit (binary_classify's strict > scan); logits (BS_STEP_LOGITS) are fp32 [B][n_labels].
+ * desc->n_labels in [1, 64] (the reference reads 2).  The stage holds word_embeddings only if it is also first;
+ * no head slice, no top-k sampling. */
+#define BS_FLAG_CLASSIFIER 2
 
 typedef struct bs_stage_desc {
   /* model (HF BloomConfig fields) */
@@ -92,6 +107,7 @@ typedef struct bs_stage_desc {
   int32_t head_vocab_begin;
   int32_t head_vocab_end;
   int32_t flags;         /* BS_FLAG_* (0 = none) */
+  int32_t n_labels;      /* BS_FLAG_CLASSIFIER: classes of the score head (else ignored) */
 } bs_stage_desc;
 
 typedef struct bs_stage bs_stage;
@@ -133,9 +149,10 @@ int bs_weights_file_probe(const char *path, int32_t *hidden, int32_t *n_layer, i
  * stage from one stream to another must order the new stream behind the old one (an event wait);
  * the library then re-writes every row's position on the new stream itself.
  *  in : first stage -> int32 token ids [B][S]; otherwise fp32 hidden [B][S][hidden]
- *  out: last stage  -> int32 token ids [B] (greedy argmax of each row's last position);
- *       otherwise fp32 hidden [B][S][hidden]
- *  logits: fp32 [B][vocab] when step->flags & BS_STEP_LOGITS (last stage only), else NULL.
+ *  out: last stage  -> int32 token ids [B] (greedy argmax of each row's last position; a BS_FLAG_CLASSIFIER
+ *       stage: int32 class ids [B]); otherwise fp32 hidden [B][S][hidden]
+ *  logits: fp32 [B][vocab] ([B][n_labels] on a classifier) when step->flags & BS_STEP_LOGITS (last stage
+ *       only), else NULL.
  * Appends S positions to KV rows [slot, slot+B): row b's new positions are p_b .. p_b+S-1 with
  * p_b = past_lens[b] (or past_len).  The last stage's token pick is greedy argmax unless
  * bs_set_sampling selected top-k sampling. */
@@ -191,9 +208,10 @@ const char *bs_last_error(void);
 /* Introspection */
 int bs_stage_info(const bs_stage *stage, bs_stage_desc *out_desc, uint64_t *weight_bytes,
                   uint64_t *kv_bytes, uint64_t *workspace_bytes);
-/* fp32 count for BS_WEIGHTS_HOST.  Canonical order: [word_embeddings if first or last]
+/* fp32 count for BS_WEIGHTS_HOST.  Canonical order: [word_embeddings if first, or last and not a classifier]
  * [emb LN g,b if first]{per layer: ln1 g,b, qkv w,b, dense w,b, ln2 g,b, fc1 w,b, fc2 w,b}
- * [ln_f g,b if last][head slice rows if a slice is set and the stage is neither first nor last]
+ * [ln_f g,b if last][score [n_labels][hidden] if a classifier]
+ * [head slice rows if a slice is set and the stage is neither first nor last]
  * [ln_f g,b if a slice is set and the stage is not last]. */
 uint64_t bs_stage_weight_count(const bs_stage_desc *desc);
 int bs_abi_version(void);
@@ -244,6 +262,11 @@ int64_t bs_codec_serialize(const bs_tensor_view *tensors, int32_t n, void *out, 
 int bs_codec_deserialize(const void *bytes, uint64_t len, bs_tensor_view *views, int32_t max_views,
                          int32_t *n_out);
 int64_t bs_dtype_size(int32_t dtype);
+/* binaryClassify(byte[]) (native-lib.cpp:128-160): the first tensor of a wire buffer holds logits; *cls = the
+ * first index of the larger of its first two floats (inference::binary_classify, inference.cpp:57-69).  Host
+ * only.  BS_ERR_INVALID for an unparsable buffer, no tensor, a non-float tensor or fewer than two elements
+ * (the reference returns -1 / -2 there, or reads past a short tensor). */
+int bs_binary_classify(const void *bytes, uint64_t len, int32_t *cls);
 /* 4-byte native (little-endian) int, as the tail stage returns a token id. */
 void bs_serialize_int(int32_t value, uint8_t out[4]);
 int bs_deserialize_int(const uint8_t *bytes, uint64_t len, int32_t *value);

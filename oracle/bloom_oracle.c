@@ -52,6 +52,8 @@ typedef struct or_stage {
   int lb, le, first, last, bf16;
   int max_batch, max_ctx;
   float *wemb, *emb_g, *emb_b, *lnf_g, *lnf_b;
+  int n_labels;   /* > 0: sequence-classification tail (or_set_classifier) */
+  float *score;   /* [n_labels][h] */
   or_layer *layers;
   float *kv;      /* [L_s][2][max_batch][nh][max_ctx][hd] */
   float *slopes;  /* [nh] */
@@ -135,6 +137,19 @@ or_stage *or_create(int hidden, int n_head, int n_layer, int vocab, float eps, i
   return s;
 }
 
+/* Sequence-classification tail (include/bloomstage.h BS_FLAG_CLASSIFIER): the last stage's head becomes
+ * score [n_labels][h] (generator tensor GT_SCORE, model level), HF BloomForSequenceClassification's
+ * `score = nn.Linear(hidden, num_labels, bias=False)`; the reference runs such a tail through
+ * run_inference_with_binary_classification (inference.cpp:220-270) behind
+ * runInferenceWorkerResidualLastClassification (native-lib.cpp:1305-1366).  Needs is_last. */
+int or_set_classifier(or_stage *s, int n_labels, uint64_t seed) {
+  if (!s || !s->last || n_labels < 1) return -1;
+  free(s->score);
+  s->score = gen_tensor(seed, -1, GT_SCORE, (size_t)n_labels * s->h, 0, s->bf16);
+  s->n_labels = n_labels;
+  return 0;
+}
+
 /* ---- Weight-only int8 (the reference's bloom*-int8 variants, server.py:796-799; the rule is
  * include/bloomstage.h BS_FLAG_INT8_WEIGHTS, whose device side is kernels.hip
  * quantize_rows_kernel).  The reference's int8 ONNX files come from the absent model_card export
@@ -172,7 +187,7 @@ int or_quantize_int8(or_stage *s) {
 
 void or_destroy(or_stage *s) {
   if (!s) return;
-  free(s->wemb); free(s->emb_g); free(s->emb_b); free(s->lnf_g); free(s->lnf_b);
+  free(s->wemb); free(s->emb_g); free(s->emb_b); free(s->lnf_g); free(s->lnf_b); free(s->score);
   int L = s->le - s->lb;
   for (int i = 0; i < L; i++) {
     or_layer *w = &s->layers[i];
@@ -389,7 +404,25 @@ int or_forward(or_stage *s, int B, int S, int slot, int past_len, const void *in
     for (size_t i = 0; i < (size_t)M * h; i++) x[i] = x[i] + a[i];
   }
 
-  if (s->last) {
+  if (s->last && s->n_labels > 0) {
+    /* sequence-classification tail: ln_f on each row's last position (the pooled token of
+     * BloomForSequenceClassification.forward for an unpadded row), score (no bias), and the first index of the
+     * largest logit (inference.cpp:57-69 binary_classify: a strict > scan keeps the first maximum) */
+    for (int b = 0; b < B; b++)
+      memcpy(a + (size_t)b * h, x + ((size_t)b * S + S - 1) * h, sizeof(float) * h);
+    layernorm(a, xn, B, h, s->lnf_g, s->lnf_b, s->eps, 1, s);
+    const int nl = s->n_labels;
+    float *lg = logits ? logits : (float *)malloc(sizeof(float) * (size_t)B * nl);
+    linear(xn, s->score, NULL, lg, B, nl, h);
+    int32_t *cls = (int32_t *)out;
+    for (int b = 0; b < B; b++) {
+      const float *r = lg + (size_t)b * nl;
+      int best = 0;
+      for (int c = 1; c < nl; c++) if (r[c] > r[best]) best = c;
+      cls[b] = best;
+    }
+    if (!logits) free(lg);
+  } else if (s->last) {
     /* ln_f on the last position of each row, tied lm_head, argmax */
     for (int b = 0; b < B; b++)
       memcpy(a + (size_t)b * h, x + ((size_t)b * S + S - 1) * h, sizeof(float) * h);

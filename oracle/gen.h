@@ -23,7 +23,7 @@
 #define GEN_U010 0x1.99999ap-28f /* 0.1  / 2^24 */
 
 /* tensor ids, model level (layer = -1) */
-enum { GT_WEMB = 0, GT_EMB_G = 1, GT_EMB_B = 2, GT_LNF_G = 3, GT_LNF_B = 4, GT_PROMPT = 255 };
+enum { GT_WEMB = 0, GT_EMB_G = 1, GT_EMB_B = 2, GT_LNF_G = 3, GT_LNF_B = 4, GT_SCORE = 5, GT_PROMPT = 255 };
 /* tensor ids, per layer */
 enum {
   GT_LN1_G = 0, GT_LN1_B, GT_QKV_W, GT_QKV_B, GT_DENSE_W, GT_DENSE_B,
@@ -76,7 +76,7 @@ static inline int gen_layer_kind(int tid) {
 }
 static inline int gen_model_kind(int tid) {
   switch (tid) {
-    case GT_WEMB: return 0;
+    case GT_WEMB: case GT_SCORE: return 0;
     case GT_EMB_G: case GT_LNF_G: return 2;
     default: return 3;
   }

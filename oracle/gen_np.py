@@ -12,7 +12,7 @@ NSC = np.float32(float.fromhex("0x1.1bc77ap-22"))
 U002 = np.float32(float.fromhex("0x1.47ae14p-30"))
 U010 = np.float32(float.fromhex("0x1.99999ap-28"))
 
-GT_WEMB, GT_EMB_G, GT_EMB_B, GT_LNF_G, GT_LNF_B, GT_PROMPT = 0, 1, 2, 3, 4, 255
+GT_WEMB, GT_EMB_G, GT_EMB_B, GT_LNF_G, GT_LNF_B, GT_SCORE, GT_PROMPT = 0, 1, 2, 3, 4, 5, 255
 (GT_LN1_G, GT_LN1_B, GT_QKV_W, GT_QKV_B, GT_DENSE_W, GT_DENSE_B,
  GT_LN2_G, GT_LN2_B, GT_FC1_W, GT_FC1_B, GT_FC2_W, GT_FC2_B) = range(12)
 
@@ -80,7 +80,7 @@ def layer_kind(tid: int) -> int:
 
 
 def model_kind(tid: int) -> int:
-    return {GT_WEMB: 0, GT_EMB_G: 2, GT_LNF_G: 2}.get(tid, 3)
+    return {GT_WEMB: 0, GT_SCORE: 0, GT_EMB_G: 2, GT_LNF_G: 2}.get(tid, 3)
 
 
 def tensor(seed: int, layer: int, tid: int, shape, chunk=1 << 24) -> np.ndarray:
@@ -115,8 +115,9 @@ def layer_shapes(h: int):
     }
 
 
-def hf_state_dict(seed: int, hidden: int, n_layer: int, vocab: int, bf16: bool = False):
-    """State dict for transformers' BloomForCausalLM built from the generator."""
+def hf_state_dict(seed: int, hidden: int, n_layer: int, vocab: int, bf16: bool = False, n_labels: int = 0):
+    """State dict for transformers' BloomForCausalLM built from the generator; with n_labels > 0 also the
+    sequence-classification head "score.weight" [n_labels][hidden] (BloomForSequenceClassification)."""
     rnd = bf16_round if bf16 else (lambda a: a)
     sd = {
         "transformer.word_embeddings.weight": rnd(tensor(seed, -1, GT_WEMB, (vocab, hidden))),
@@ -137,6 +138,8 @@ def hf_state_dict(seed: int, hidden: int, n_layer: int, vocab: int, bf16: bool =
         for tid, shape in layer_shapes(hidden).items():
             sd[f"transformer.h.{l}.{names[tid]}"] = rnd(tensor(seed, l, tid, shape))
     sd["lm_head.weight"] = sd["transformer.word_embeddings.weight"]
+    if n_labels:
+        sd["score.weight"] = rnd(tensor(seed, -1, GT_SCORE, (n_labels, hidden)))
     return sd
 
 

@@ -34,6 +34,8 @@ def lib():
         L.or_set_emul_pv.argtypes = [ctypes.c_int]
         L.or_round_fp16.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
         L.or_set_skip_round.argtypes = [ctypes.c_int]
+        L.or_set_classifier.restype = ctypes.c_int
+        L.or_set_classifier.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]
         L.or_quantize_int8.restype = ctypes.c_int
         L.or_quantize_int8.argtypes = [ctypes.c_void_p]
         L.or_head_norm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -104,8 +106,12 @@ class OracleStage:
     """CPU checker for one pipeline stage; same call semantics as the product Stage."""
 
     def __init__(self, hidden, n_head, n_layer, vocab, layer_begin, layer_end, *, bf16=False,
-                 max_batch=1, max_ctx=64, seed=0, eps=1e-5, is_first=None, is_last=None, int8=False, emul_pv=None):
+                 max_batch=1, max_ctx=64, seed=0, eps=1e-5, is_first=None, is_last=None, int8=False, emul_pv=None,
+                 n_labels=0):
+        """n_labels > 0: a sequence-classification tail (or_set_classifier): the last stage emits class ids and
+        fp32 logits [B][n_labels] instead of tokens and vocabulary logits."""
         self.hidden, self.vocab = hidden, vocab
+        self.n_out = n_labels if n_labels else vocab
         self.emul = emul_pv  # None: the global knob as set (checker_mode); else this stage's own P.V mode per call
         self.is_first = layer_begin == 0 if is_first is None else is_first
         self.is_last = layer_end == n_layer if is_last is None else is_last
@@ -115,13 +121,15 @@ class OracleStage:
             raise ValueError("or_create failed (bad stage description)")
         if int8 and lib().or_quantize_int8(self.h) != 0:  # weight-only int8 (BS_FLAG_INT8_WEIGHTS)
             raise ValueError("or_quantize_int8 needs a bf16-mode stage")
+        if n_labels and lib().or_set_classifier(self.h, n_labels, seed) != 0:
+            raise ValueError("or_set_classifier needs a last stage and n_labels >= 1")
 
     def forward(self, x, B, S, slot=0, past_len=0, want_logits=False):
         if self.is_first:
             x = np.ascontiguousarray(x, dtype=np.int32).reshape(B, S)
         else:
             x = np.ascontiguousarray(x, dtype=np.float32).reshape(B, S, self.hidden)
-        logits = np.empty((B, self.vocab), dtype=np.float32) if (self.is_last and want_logits) else None
+        logits = np.empty((B, self.n_out), dtype=np.float32) if (self.is_last and want_logits) else None
         out = np.empty(B, dtype=np.int32) if self.is_last else np.empty((B, S, self.hidden), dtype=np.float32)
         if self.emul is None:
             rc = lib().or_forward(self.h, B, S, slot, past_len, _p(x), _p(out), _p(logits))

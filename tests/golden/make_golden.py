@@ -20,7 +20,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", ".."))
 from oracle import gen_np  # noqa: E402
 
-from transformers import BloomConfig, BloomForCausalLM  # noqa: E402
+from transformers import BloomConfig, BloomForCausalLM, BloomForSequenceClassification  # noqa: E402
 from transformers.models.bloom.modeling_bloom import build_alibi_tensor  # noqa: E402
 
 torch.set_grad_enabled(False)
@@ -116,6 +116,28 @@ def family_blocks():
     np.savez_compressed(os.path.join(HERE, "family_blocks.npz"), **out)
 
 
+def tiny_classify():
+    """(4) sequence-classification tail: BloomForSequenceClassification's pooled logits (the row's last
+    non-pad token; no prompt holds the pad id) and their argmax, for 2 labels (what the reference's
+    binary_classify reads, inference.cpp:57-69) and 3 labels."""
+    h, nh, L, V, seed, B, S = 64, 4, 2, 512, 3, 3, 9
+    ids = gen_np.prompt_ids(4321, B, S, V)
+    out = {"config": np.array([h, nh, L, V, seed, B, S]), "ids": ids.astype(np.int32)}
+    for nl in (2, 3):
+        pad = next(p for p in range(V) if not (ids == p).any())
+        cfg = BloomConfig(vocab_size=V, hidden_size=h, n_layer=L, n_head=nh, layer_norm_epsilon=1e-5,
+                          hidden_dropout=0.0, attention_dropout=0.0, num_labels=nl, pad_token_id=pad)
+        m = BloomForSequenceClassification(cfg).eval().float()
+        sd = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in
+              gen_np.hf_state_dict(seed, h, L, V, n_labels=nl).items() if k != "lm_head.weight"}
+        m.load_state_dict(sd, strict=True)
+        lg = m(input_ids=torch.from_numpy(ids)).logits.numpy()
+        out[f"logits{nl}"] = lg
+        out[f"class{nl}"] = lg.argmax(-1).astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "tiny_classify.npz"), **out)
+    print("tiny_classify ok")
+
+
 def alibi():
     """(3) ALiBi slopes from HF build_alibi_tensor for 16, 32 and 12 heads."""
     res = {}
@@ -131,3 +153,4 @@ if __name__ == "__main__":
     tiny_e2e()
     tiny_nonpow2()
     family_blocks()
+    tiny_classify()

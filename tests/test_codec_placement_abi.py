@@ -111,6 +111,38 @@ def test_weight_count_matches_canonical_layout():
     assert bad == 0
 
 
+def test_weight_count_classifier_tail():
+    """BS_FLAG_CLASSIFIER: a last-only classifier stage holds no word_embeddings, ln_f and score [n_labels][h];
+    a whole-model classifier keeps the embedding (it is first).  Bad n_labels / non-last stages / head slices
+    are rejected (count 0)."""
+    h, V = 64, 512
+    kw = dict(hidden=h, n_head=4, n_layer=4, vocab=V, ln_eps=1e-5, dtype=16, max_batch=1, max_ctx=8,
+              flags=bs.BS_FLAG_CLASSIFIER)
+    assert bs.weight_count(layer_begin=2, layer_end=4, is_first=0, is_last=1, n_labels=2, **kw) == \
+        2 * (12 * h * h + 13 * h) + 2 * h + 2 * h
+    assert bs.weight_count(layer_begin=0, layer_end=4, is_first=1, is_last=1, n_labels=3, **kw) == \
+        V * h + 2 * h + 4 * (12 * h * h + 13 * h) + 2 * h + 3 * h
+    assert bs.weight_count(layer_begin=2, layer_end=4, is_first=0, is_last=1, n_labels=0, **kw) == 0
+    assert bs.weight_count(layer_begin=2, layer_end=4, is_first=0, is_last=1, n_labels=65, **kw) == 0
+    assert bs.weight_count(layer_begin=0, layer_end=2, is_first=1, is_last=0, n_labels=2, **kw) == 0
+    assert bs.weight_count(layer_begin=2, layer_end=4, is_first=0, is_last=1, n_labels=2, head_vocab_begin=0,
+                           head_vocab_end=64, **kw) == 0
+
+
+def test_binary_classify_on_wire_bytes():
+    """binaryClassify (native-lib.cpp:128-160): first tensor = logits, first index of the larger of the first
+    two floats (inference.cpp:57-69); ties keep index 0; errors instead of the reference's -1 / -2 / over-read."""
+    assert bs.binary_classify(bs.serialize_tensors([np.array([[0.1, 0.7]], np.float32)])) == 1
+    assert bs.binary_classify(bs.serialize_tensors([np.array([[0.7, 0.1, 9.0]], np.float32)])) == 0
+    assert bs.binary_classify(bs.serialize_tensors([np.array([0.5, 0.5], np.float32), np.ones(3, np.int64)])) == 0
+    assert bs.binary_classify(bs.serialize_tensors([np.array([-np.inf, -1e30], np.float32)])) == 1
+    for bad in ([], [np.array([1.0], np.float32)], [np.array([1, 2], np.int32)]):
+        with pytest.raises(bs.BloomStageError):
+            bs.binary_classify(bs.serialize_tensors(bad))
+    with pytest.raises(bs.BloomStageError):
+        bs.binary_classify(b"\x01\x00")
+
+
 def test_init_without_gpu_fails_loudly():
     import torch
     if torch.cuda.is_available():

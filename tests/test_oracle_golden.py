@@ -124,3 +124,28 @@ def test_bf16_noise_floor_of_the_checker():
     d = float(np.abs(outs[0] - outs[1]).max())
     scale = float(np.abs(outs[1]).max())
     assert 1e-3 < d < 2.5e-3 * scale, (d, scale)
+
+
+@pytest.mark.parametrize("n_labels", [2, 3])
+@pytest.mark.parametrize("split", [0, 1])
+def test_classifier_tail_matches_hf(n_labels, split):
+    """Sequence-classification tail (or_set_classifier) against BloomForSequenceClassification's pooled logits,
+    as one stage and as a 1 + 1 layer split; the class is the first maximal index (inference.cpp:57-69)."""
+    g = _load("tiny_classify.npz")
+    h, nh, L, V, seed, B, S = (int(v) for v in g["config"])
+    x = g["ids"]
+    if split:
+        x = OracleStage(h, nh, L, V, 0, split, max_batch=B, max_ctx=S, seed=seed).forward(x, B, S)
+    st = OracleStage(h, nh, L, V, split, L, max_batch=B, max_ctx=S, seed=seed, n_labels=n_labels)
+    cls, lg = st.forward(x, B, S, want_logits=True)
+    ref = g[f"logits{n_labels}"]
+    assert lg.shape == (B, n_labels)
+    np.testing.assert_allclose(lg, ref, atol=2e-6 * np.abs(ref).max(), rtol=0)
+    assert np.array_equal(cls, g[f"class{n_labels}"])
+
+
+def test_classifier_one_label():
+    """n_labels = 1 (a regression-style head): logits [B][1], every row's class 0."""
+    st = OracleStage(64, 4, 1, 512, 0, 1, max_batch=2, max_ctx=4, seed=1, n_labels=1)
+    cls, lg = st.forward(np.array([[5, 6], [7, 8]]), 2, 2, want_logits=True)
+    assert lg.shape == (2, 1) and np.array_equal(cls, [0, 0])
