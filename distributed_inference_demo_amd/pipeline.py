@@ -325,6 +325,21 @@ def generate(pipe: Pipeline, prompt, steps, prompt_len):
     return torch.cat([torch.stack(r, 1) for r in rec], 0)
 
 
+def classify(pipe: Pipeline, prompt, prompt_len):
+    """The reference's classification task (max_length == 0: one OneStep pass per sample, Communication.java:591-603,
+    the tail running runInferenceWorkerResidualLastClassification, native-lib.cpp:1305-1366): one pipeline pass of
+    `prompt` [n_mb*mb, prompt_len] (rank 0; None elsewhere) from empty KV rows through a pipeline whose last stage
+    is a classifier (build_rank(..., n_labels=...)).  Rank 0 returns the class ids [n_mb*mb]; other ranks None.
+    Collective: every rank calls it."""
+    pipe.past = [0] * pipe.n_mb  # every pass classifies new samples
+    rec = [[] for _ in range(pipe.n_mb)] if pipe.is_first else None
+    pipe.step(prompt_len, prompt=prompt, record=rec)
+    pipe.finish(record=rec)
+    if not pipe.is_first:
+        return None
+    return torch.cat([r[-1] for r in rec], 0)
+
+
 def init_distributed(backend=None, timeout_s=None):
     """Read RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* (torchrun) and initialise the process group.  Every
     collective and point-to-point wait is bounded by `timeout_s` (env BS_PIPELINE_TIMEOUT_S, default
@@ -387,10 +402,14 @@ def connect_p2p(rank, world, head_split, groups, device):
 
 
 def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb_rows=1, n_mb=None, max_ctx=1024,
-               max_seq=512, seed=0, head_split=None, executor_factory=None):
+               max_seq=512, seed=0, head_split=None, executor_factory=None, n_labels=0):
     """Create this rank's stage (server.py:893-905 layer range, plus a vocabulary slice of the
-    tied lm_head when head_split) and its Pipeline.  Collective: every rank must call it."""
-    head_split = (world > 1) if head_split is None else (head_split and world > 1)
+    tied lm_head when head_split) and its Pipeline.  n_labels > 0: the last stage is a sequence-classification
+    tail (BS_FLAG_CLASSIFIER; `classify` runs the task) and there is no head ring.  Collective: every rank must
+    call it."""
+    if n_labels and head_split:
+        raise ValueError("a classifier tail holds its own score head: no vocabulary-parallel head ring")
+    head_split = (world > 1 and not n_labels) if head_split is None else (head_split and world > 1)
     n_mb = (2 * world if head_split else world) if n_mb is None else n_mb
     if world > model.n_layer:
         raise ValueError(f"{world} stages for {model.n_layer} layers: every stage needs at least one layer")
@@ -407,10 +426,12 @@ def build_rank(model: config.BloomDims, rank, world, device, *, dtype="bf16", mb
         st = Stage(model.hidden, model.n_head, model.n_layer, model.vocab, lb, le, dtype=dtype,
                    device=device.index if device.type == "cuda" else 0, max_batch=mb_rows * n_mb,
                    max_ctx=max_ctx, max_tokens=mb_rows * max_seq, seed=seed, is_first=is_first,
-                   is_last=is_last and not head_split, head_slice=hslice, int8_weights=model.int8_weights)
+                   is_last=is_last and not head_split, head_slice=hslice, int8_weights=model.int8_weights,
+                   n_labels=n_labels if is_last else 0)
         ex = StageExecutor(st)
     else:
-        ex = executor_factory(lb, le, is_first, is_last and not head_split, mb_rows * n_mb, max_ctx, hslice)
+        kw = {"n_labels": n_labels} if (n_labels and is_last) else {}
+        ex = executor_factory(lb, le, is_first, is_last and not head_split, mb_rows * n_mb, max_ctx, hslice, **kw)
     # communicators are created collectively, in the same order on every rank
     tok_group = head_group = pf_group = None
     if world > 1:

@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from distributed_inference_demo_amd import config
-from distributed_inference_demo_amd.pipeline import build_rank, generate
+from distributed_inference_demo_amd.pipeline import build_rank, classify, generate
 from oracle.oracle import OracleStage, prompt_ids
 
 MODEL = config.BloomDims("tiny", 64, 4, 4, vocab=512)
@@ -24,10 +24,10 @@ SEED, P, STEPS, MB = 3, 6, 10, 2
 
 
 class OracleExecutor:
-    def __init__(self, lb, le, first, last, max_batch, max_ctx, hslice=None, model=MODEL):
+    def __init__(self, lb, le, first, last, max_batch, max_ctx, hslice=None, model=MODEL, n_labels=0):
         self.model = model
         self.st = OracleStage(model.hidden, model.n_head, model.n_layer, model.vocab, lb, le, max_batch=max_batch,
-                              max_ctx=max_ctx, seed=SEED, is_first=first, is_last=last)
+                              max_ctx=max_ctx, seed=SEED, is_first=first, is_last=last, n_labels=n_labels)
         self.first, self.last, self.hslice = first, last, hslice
         if hslice is not None:  # layer-free stage owning the tied head for ln_f + the vocab slice
             self.head = OracleStage(model.hidden, model.n_head, model.n_layer, model.vocab, 0, 0, max_batch=max_batch,
@@ -55,11 +55,24 @@ class OracleExecutor:
         out.copy_(torch.from_numpy(np.ascontiguousarray(y).reshape(-1)[: out.numel()]).view(out.shape))
 
 
-def _worker(rank, world, port, q, head_split=False, resume=0, model=MODEL):
+def _worker(rank, world, port, q, head_split=False, resume=0, model=MODEL, n_labels=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       OMP_NUM_THREADS="1")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        if n_labels:  # classification: two passes of new samples (KV rows reused from position 0)
+            pipe, rng = build_rank(model, rank, world, torch.device("cpu"), mb_rows=MB, max_ctx=P, max_seq=P,
+                                   executor_factory=functools.partial(OracleExecutor, model=model), dtype="fp32",
+                                   n_labels=n_labels)
+            q.put(("range", rank, rng, pipe.n_mb))
+            out = []
+            for seed in (1234, 99):
+                prompt = torch.from_numpy(prompt_ids(seed, MB * pipe.n_mb, P, model.vocab)) if rank == 0 else None
+                out.append(classify(pipe, prompt, P))
+            if rank == 0:
+                q.put(("tokens", torch.stack(out).numpy()))
+            dist.barrier()
+            return
         pipe, rng = build_rank(model, rank, world, torch.device("cpu"), mb_rows=MB, max_ctx=P + STEPS + resume + 2,
                                max_seq=P, executor_factory=functools.partial(OracleExecutor, model=model),
                                head_split=head_split, dtype="fp32")
@@ -88,12 +101,13 @@ def _free_port():
     return p
 
 
-def _run(world, head_split, resume, model=MODEL):
+def _run(world, head_split, resume, model=MODEL, n_labels=0):
     """Spawn `world` gloo ranks; returns (rank 0's tokens, {rank: (layer range, micro-batches)})."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, head_split, resume, model)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, head_split, resume, model, n_labels))
+             for r in range(world)]
     for p in procs:
         p.start()
     got, ranges = None, {}
@@ -148,6 +162,20 @@ def test_pipeline_matches_single_stage(world, head_split, resume):
     assert np.array_equal(got, np.stack(want, 1))
 
 
+@pytest.mark.parametrize("world", [1, 3])
+def test_pipeline_classification_matches_single_stage(world):
+    """Classification task (max_length == 0, Communication.java:591-603): one pass of new samples through the
+    stages, the last a classifier tail; the class ids equal one whole-model classifier stage's, pass after pass."""
+    n_labels = 3
+    got, _ = _run(world, False, 0, n_labels=n_labels)
+    B = got.shape[1]
+    for i, seed in enumerate((1234, 99)):
+        ref = OracleStage(MODEL.hidden, MODEL.n_head, MODEL.n_layer, MODEL.vocab, 0, MODEL.n_layer, max_batch=B,
+                          max_ctx=P, seed=SEED, n_labels=n_labels)
+        assert np.array_equal(got[i], ref.forward(prompt_ids(seed, B, P, MODEL.vocab), B, P))
+    assert got.min() >= 0 and got.max() < n_labels
+
+
 def test_build_rank_rejects_unplaceable_splits():
     """More stages than layers (an empty stage), more head slices than 16-column tiles, and an
     int8 model in fp32 are configuration errors, raised before any stage is built."""
@@ -159,6 +187,8 @@ def test_build_rank_rejects_unplaceable_splits():
         build_rank(narrow, 0, 5, cpu, executor_factory=OracleExecutor, dtype="fp32", head_split=True)
     with pytest.raises(ValueError, match="int8"):
         build_rank(config.get("bloom560m-int8"), 0, 1, cpu, executor_factory=OracleExecutor, dtype="fp32")
+    with pytest.raises(ValueError, match="classifier"):
+        build_rank(MODEL, 0, 2, cpu, executor_factory=OracleExecutor, dtype="fp32", head_split=True, n_labels=2)
 
 
 def test_single_rank_pipeline_loops_tokens_back():
