@@ -556,19 +556,24 @@ __device__ __forceinline__ void ln_rows_finish(const LnArgs& ln, int M, int K, f
   __syncthreads();
 }
 
-// LayerNorm of M fp32 rows (K <= 4096, K % 4 == 0) -> bf16 with ONE WAVE per row (a 64-thread block): the row in
-// registers (NV float4 per lane), the shifted-sum statistics of ln_rows_finish by DPP wave reductions -- no LDS
-// and no barrier (round 4; the 256-thread block per row paid two block barriers for 6 KB of row).
-template <int NV>
-__global__ __launch_bounds__(64) void ln_rows_wave_kernel(LnArgs ln, int K, bf16* __restrict__ out) {
-  const int lane = threadIdx.x;
+// LayerNorm of M fp32 rows (K <= 4096, K % 4 == 0) -> bf16 with WPR waves per row (a 64 * WPR-thread block): the row
+// in registers (NV float4 per lane; lane l of wave w holds float4 groups i * 64 * WPR + w * 64 + l), the shifted-sum
+// statistics of ln_rows_finish by DPP wave reductions, and for WPR > 1 one LDS exchange of the WPR wave sums (added in
+// wave order).  Round 4 went from a 256-thread block per row (two block barriers) to one wave per row; round 6
+// measured one wave per row latency-bound at wide rows (tools/ln_bench.hip, profiles/r06_ln_rows_ab.txt: bloom-7b1
+// K = 4096 4.9-5.1 us, 4 waves per row 2.8-3.0 us; 3b 3.9 -> 2.7; 1b1 2.8-3.0 -> 2.6-2.7), so rows wider than 1024
+// take 4 waves.
+template <int NV, int WPR>
+__global__ __launch_bounds__(64 * WPR) void ln_rows_wave_kernel(LnArgs ln, int K, bf16* __restrict__ out) {
+  __shared__ float sh[2 * WPR];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float* xr = ln.x + (size_t)blockIdx.x * ln.row_stride * K + (size_t)ln.row_offset * K;
   float4 xv[NV];
   uint2 gr[NV], br[NV];
   const float c = xr[0];
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    const int k = (i * 64 + lane) * 4;
+    const int k = (i * 64 * WPR + w * 64 + lane) * 4;
     xv[i] = k < K ? *reinterpret_cast<const float4*>(xr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
     gr[i] = k < K ? *reinterpret_cast<const uint2*>(ln.gamma + k) : make_uint2(0u, 0u);
     br[i] = k < K ? *reinterpret_cast<const uint2*>(ln.beta + k) : make_uint2(0u, 0u);
@@ -576,19 +581,28 @@ __global__ __launch_bounds__(64) void ln_rows_wave_kernel(LnArgs ln, int K, bf16
   float a1 = 0.f, a2 = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    if ((i * 64 + lane) * 4 < K) {
+    if ((i * 64 * WPR + w * 64 + lane) * 4 < K) {
       const float d0 = xv[i].x - c, d1 = xv[i].y - c, d2 = xv[i].z - c, d3 = xv[i].w - c;
       a1 += (d0 + d1) + (d2 + d3);
       a2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
     }
   }
+  a1 = wave_sum(a1);
+  a2 = wave_sum(a2);
+  if constexpr (WPR > 1) {
+    if (lane == 0) { sh[w] = a1; sh[WPR + w] = a2; }
+    __syncthreads();
+    a1 = sh[0]; a2 = sh[WPR];
+#pragma unroll
+    for (int j = 1; j < WPR; j++) { a1 += sh[j]; a2 += sh[WPR + j]; }
+  }
   const float invk = 1.0f / (float)K;
-  const float t1 = wave_sum(a1) * invk, t2 = wave_sum(a2) * invk;
+  const float t1 = a1 * invk, t2 = a2 * invk;
   const float mean = c + t1, rstd = 1.0f / sqrtf(fmaxf(t2 - t1 * t1, 0.f) + ln.eps);
   bf16* orow = out + (size_t)blockIdx.x * K;
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    const int k = (i * 64 + lane) * 4;
+    const int k = (i * 64 * WPR + w * 64 + lane) * 4;
     if (k < K) {
       float4 g, b;
       bf16x4_to_f32(gr[i], g);
@@ -604,12 +618,15 @@ __global__ __launch_bounds__(64) void ln_rows_wave_kernel(LnArgs ln, int K, bf16
   }
 }
 
-// K <= 4096, K % 4 == 0: one wave per row, NV = ceil(K / 256) float4 per lane.
+// K <= 4096, K % 4 == 0: one wave per row up to K = 1024 (NV = K / 256 float4 per lane), 4 waves per row above.
 static void launch_ln_rows_wave(const LnArgs& ln, int M, int K, bf16* out, hipStream_t s) {
-  const int nv = (K + 255) / 256;
-  if (nv <= 4) ln_rows_wave_kernel<4><<<M, 64, 0, s>>>(ln, K, out);
-  else if (nv <= 8) ln_rows_wave_kernel<8><<<M, 64, 0, s>>>(ln, K, out);
-  else ln_rows_wave_kernel<16><<<M, 64, 0, s>>>(ln, K, out);
+  if (K <= 1024) {
+    ln_rows_wave_kernel<4, 1><<<M, 64, 0, s>>>(ln, K, out);
+    return;
+  }
+  const int nv = (K + 1023) / 1024;
+  if (nv <= 2) ln_rows_wave_kernel<2, 4><<<M, 256, 0, s>>>(ln, K, out);
+  else ln_rows_wave_kernel<4, 4><<<M, 256, 0, s>>>(ln, K, out);
 }
 
 // Diagnostic builds only (tools/gemv_timeline.hip defines BS_STAMPS): wave 0 of every block records
