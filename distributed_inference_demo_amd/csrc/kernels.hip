@@ -1461,12 +1461,28 @@ static const TileCfg kTileTable[] = {
   {4096, 4096, 1, 1, 8, 2, 2, 8},    {16384, 4096, 4, 1, 8, 4, 1, 8},  {4096, 16384, 2, 2, 8, 2, 2, 8},
 };
 
+// Token counts the batched tile GEMV (gemv_ldsw4) takes for plain and LayerNorm-fused GEMVs: M >= 3, and M = 2 on
+// K >= 2560 (bloom-3b / 7b1 widths); below, the rows GEMV.  Round 6 (tools/gpu_r6w.sh, profiles/r06_tiles_min_m_ab.txt):
+// M = 3..4 had gone to the rows GEMV (whose time grows with M: bloom-1b1 fc2 7.0 -> 10.9 us from M = 1 to 4) or the
+// old gemv_mfma; on the tile GEMV decode at B = 3 / 4 runs +28-38 % (bloom-1b1 B = 4 3122 -> 4140 tok/s, 7b1
+// 999 -> 1351), B = 2 +3 % (3b) / +11 % (7b1), while bloom-1b1 B = 2 keeps the rows GEMV (-4 % on tiles).
+// BS_TILES_MIN_M (read once) replaces the rule by a plain threshold for A/B runs.
+static bool tiles_take(int M, int K) {
+  static const int v = [] {
+    const char* e = getenv("BS_TILES_MIN_M");
+    const int m = e ? atoi(e) : 0;
+    return m >= 2 && m <= 33 ? m : 0;
+  }();
+  if (v) return M >= v;
+  return M >= 3 || (M == 2 && K >= 2560);
+}
+
 // ln != nullptr (bf16): X = LN(ln->x) fused into gemv_ldsw4's prologue when the shape takes one K split of
 // 2..5 stages per wave and M <= 16; otherwise returns false and the caller normalises first.
 template <typename WT = bf16>
 static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K, const Epi& ep, hipStream_t s,
                                 const LnArgs* ln = nullptr) {
-  if (M <= 4 || M > 32 || (K % 64) != 0) return false;
+  if (!tiles_take(M, K) || M > 32 || (K % 64) != 0) return false;
   const int units = K / 64;
   int T = N >= 16384 ? 4 : 2, KS = 1, WV = 0;
   for (const TileCfg& c : kTileTable)
@@ -2380,6 +2396,8 @@ template <int XM>
 static bool gemv_rows_dispatch(const bf16* x, const LnArgs& ln, const AttnParts& pa, const bf16* w, int M, int N,
                                int K, const Epi& ep, hipStream_t s) {
   if (M > 4 || (K % 8) != 0 || K < 8 || (XM != X_PLAIN && K > 4096)) return false;
+  // the tile GEMV takes the plain / LayerNorm-fused GEMVs of its token counts (tiles_take) when K has a tile path
+  if ((XM == X_PLAIN || XM == X_LN) && ep.kind != EPI_ARGMAX && tiles_take(M, K) && (K % 64) == 0) return false;
   // M = 3..4: rows loses to the MFMA GEMV on LN-fused and large shapes
   // (tools/gemv_bench.hip, profiles/r01_gemv_bench_m4.log); keep it for small plain GEMVs and the head
   // (and for PARTS, which only this kernel implements).
@@ -2445,9 +2463,9 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
                       const void* beta, float eps, void* xn_scratch, const void* W, int M, int N, int K,
                       const Epi& ep, hipStream_t s) {
   if (M <= 0) return;
-  // 4 < M <= 32: a LayerNorm kernel + the tile GEMV beats the per-tile LN-fused GEMV
-  // (tools/gemv_probe.hip batched section)
-  const bool tiles = is_bf16 && M > 4 && M <= 32 && (K % 64) == 0;
+  // the tile GEMV's token counts (tiles_take, up to 32): its LN-fused prologue where the shape allows it, else a
+  // LayerNorm kernel + the tile GEMV (tools/gemv_probe.hip batched section)
+  const bool tiles = is_bf16 && tiles_take(M, K) && M <= 32 && (K % 64) == 0;
   if (is_bf16 && M <= 8 && (K % 8) == 0 && !tiles) {
     LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
     gemv_dispatch<true>(nullptr, ln, (const bf16*)W, M, N, K, ep, s);
