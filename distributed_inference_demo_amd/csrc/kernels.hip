@@ -2485,7 +2485,15 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
 }
 
 bool linear_parts_supported(int M, int K, int head_dim, int nsplit) {
-  return M >= 1 && M <= 4 && K % 8 == 0 && K >= 8 && K <= 4096 && head_dim % 4 == 0 && nsplit >= 2 &&
+  // M <= 2 defers the merge to the rows GEMV's prologue; at M = 3..4 the attention's last split merges by ticket
+  // and the dense GEMV runs on the tile GEMV (round 6, profiles/r06_parts_max_m_ab.txt: 1024-token prompt, B = 4:
+  // bloom-1b1 +2 %, 3b +8 %, 7b1 +16 %; B = 2 keeps the deferral, 3b -3 % without it).  BS_PARTS_MAX_M: A/B knob.
+  static const int max_m = [] {
+    const char* e = getenv("BS_PARTS_MAX_M");
+    const int m = e ? atoi(e) : 0;
+    return m >= 1 && m <= 4 ? m : 2;
+  }();
+  return M >= 1 && M <= max_m && K % 8 == 0 && K >= 8 && K <= 4096 && head_dim % 4 == 0 && nsplit >= 2 &&
          nsplit <= kPartsMaxSplit;
 }
 
