@@ -1410,6 +1410,14 @@ static bool gemv_ldsw4_ln_launch(const LnArgs& ln, const bf16* W, int M, int N, 
   constexpr int WAVES = 8;
   const int nst = K / (WAVES * 64);
   const int mt = 1;
+  // where the fused LayerNorm beats the LayerNorm launch + plain tile GEMV (round 6, profiles/r06_lns_ab.txt): rows of
+  // K <= 1024 at every M (bloom-560m +3-7 %), K <= 1536 up to M = 8 (bloom-1b1 +1-2 %; M = 16 -1 %), not at bloom-3b's
+  // K = 2560 (-0.3 .. -4 %: every block loads all M fp32 rows).  BS_LNS_MAX_M (read once) replaces the rule.
+  static const int lns_max_m = [] {
+    const char* e = getenv("BS_LNS_MAX_M");
+    return e ? atoi(e) : -1;
+  }();
+  if (lns_max_m >= 0 ? M > lns_max_m : !(K <= 1024 || (K <= 1536 && M <= 8))) return false;
   if (M > 16 || K % (WAVES * 64) || nst < 2 || nst > 5) return false;
   // the activation descriptor's byte size and the per-row offsets are 32-bit: rows that reach 2^31 bytes (a long
   // lm_head row stride) take the LayerNorm launch instead
