@@ -2868,17 +2868,19 @@ size_t attention_workspace_floats(int B, int n_head, int head_dim, int max_ctx, 
 }
 
 // One 8-wave block per (row, head) when that already fills the chip or the cache is short;
-// otherwise 4-wave blocks split the context so ~256 blocks stream the KV cache (>= one 64-position
+// otherwise 4-wave blocks split the context so ~512 blocks stream the KV cache (>= one 64-position
 // chunk per wave at full cache).  Static per (B, n_head, cache size), so the consumer of a deferred
 // merge knows it without a device round trip.
 // A wide variant (2-wave blocks of 32 positions, one block per 64 cached positions, ticket merge in the
 // launch) measured bloom-7b1 B = 1 +1.7 %, bloom-1b1 B = 1 -4 % (profiles/r02_attn_wide_ab.txt): removed.
 // Round 4 A/B (profiles/r04_attn_decode_splits_ab.txt): 2 or 1 chunks per split instead of 4 -- more blocks
 // streaming the cache, more partials for the dense prologue to merge -- cost bloom-1b1 B = 1 3 %.
+// Round 6 (profiles/r06_attn_splits_ab.txt, 1024-token prompt): ~512 blocks instead of ~256 when the pairs are few
+// (bloom-1b1 B = 4 / 8 +1.6 / +3.8 %, 7b1 B = 4 +1.6 %); batch 1 stays bounded by the 4-chunk split length.
 int attention_decode_splits(int B, int n_head, int max_chunks) {
   const int pairs = B * n_head;
   if (pairs >= 192 || max_chunks <= 4) return 1;
-  const int nsplit = min((256 + pairs - 1) / pairs, (max_chunks + 3) / 4);
+  const int nsplit = min((512 + pairs - 1) / pairs, (max_chunks + 3) / 4);
   return max(1, min(nsplit, 64));
 }
 
