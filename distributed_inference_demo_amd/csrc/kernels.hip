@@ -2473,7 +2473,9 @@ void launch_linear_ln(int is_bf16, const float* x, int row_stride, int row_offse
   if (M <= 0) return;
   // the tile GEMV's token counts (tiles_take, up to 32): its LN-fused prologue where the shape allows it, else a
   // LayerNorm kernel + the tile GEMV (tools/gemv_probe.hip batched section)
-  const bool tiles = is_bf16 && tiles_take(M, K) && M <= 32 && (K % 64) == 0;
+  // the head (argmax) at M <= 2 keeps the rows GEMV's LayerNorm-fused argmax (profiles/r06_head_path_ab.txt: 3b / 7b1
+  // B = 2 +0.4-0.6 % over the tile path; at M = 3..4 the tile path wins 1-3 %)
+  const bool tiles = is_bf16 && tiles_take(M, K) && M <= 32 && (K % 64) == 0 && !(ep.kind == EPI_ARGMAX && M <= 2);
   if (is_bf16 && M <= 8 && (K % 8) == 0 && !tiles) {
     LnArgs ln{x, row_stride, row_offset, (const bf16*)gamma, (const bf16*)beta, eps};
     gemv_dispatch<true>(nullptr, ln, (const bf16*)W, M, N, K, ep, s);
