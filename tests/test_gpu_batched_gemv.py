@@ -115,3 +115,25 @@ def test_small_batch_decode_middle_stage_widths(h, nh, B):
                     "bf16", f"h={h} B={B} decode step {step}")
     gs.close()
     os_.close()
+
+
+@pytest.mark.parametrize("h,nh", [(2560, 32), (4096, 32)])
+@pytest.mark.parametrize("B", [2, 3, 4])
+def test_two_to_four_rows_decode_split_attention(h, nh, B):
+    """2 <= B <= 4 at the 3b / 7b1 widths after a 260-token prefill (round-6 dispatch): the tile GEMV takes M = 3..4
+    everywhere and M = 2 at these K; the split decode attention (2 splits at this cache size) merges its own partials
+    at M = 3..4 and defers the merge to the dense rows GEMV at M = 2.  One middle layer, 3 decode steps."""
+    from test_gpu_parity import check_close as _cc
+    check_close = (lambda g, o, dt, what: check_h4096_hidden(g, o, what)) if h == 4096 else _cc
+    L, V, P = 2, 1024, 260
+    gs, os_ = pair(h, nh, L, V, 1, 2, "bf16", seed=43, max_batch=B, max_ctx=400, max_tokens=B * P, is_first=False,
+                   is_last=False)
+    rng = np.random.default_rng(11)
+    x = (rng.standard_normal((B, P, h))).astype(np.float32)
+    check_close(gs.forward_host(x, B, P, past_len=0), os_.forward(x, B, P, past_len=0), "bf16", f"h={h} B={B} prefill")
+    for step in range(3):
+        x1 = rng.standard_normal((B, 1, h)).astype(np.float32)
+        check_close(gs.forward_host(x1, B, 1, past_len=P + step), os_.forward(x1, B, 1, past_len=P + step), "bf16",
+                    f"h={h} B={B} decode step {step}")
+    gs.close()
+    os_.close()
