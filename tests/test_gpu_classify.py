@@ -135,3 +135,24 @@ def test_classifier_rejects_generation_only_calls():
         st.set_sampling(4)
     with pytest.raises(BloomStageError):
         Stage(64, 4, 2, 512, 0, 1, dtype="bf16", max_ctx=8, seed=1, is_last=False, n_labels=2)
+
+
+def test_classifier_tail_with_int8_block_weights():
+    """BS_FLAG_CLASSIFIER with BS_FLAG_INT8_WEIGHTS (the reference's bloom*-int8 modules, server.py:796-799): the block
+    matrices run the int8 GEMVs / GEMMs, the score head stays bf16; against the checker's int8 restatement with the same
+    classifier head (prefill then decode-shaped steps)."""
+    h, nh, L, V, B, S, nl = 256, 4, 2, 1024, 2, 12, 3
+    g = Stage(h, nh, L, V, 1, L, dtype="bf16", max_batch=B, max_ctx=32, seed=17, n_labels=nl, int8_weights=True)
+    o = OracleStage(h, nh, L, V, 1, L, bf16=True, max_batch=B, max_ctx=32, seed=17, n_labels=nl, int8=True)
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((B, S, h)).astype(np.float32)
+    cg, lg = g.forward_host(x, B, S, want_logits=True)
+    co, lo = o.forward(x, B, S, want_logits=True)
+    check_logits(lg, lo, "bf16", "int8 classifier prefill")
+    assert_ids_match(cg, co, lo, "int8 classifier prefill")
+    for step in range(3):
+        x1 = rng.standard_normal((B, 1, h)).astype(np.float32)
+        cg, lg = g.forward_host(x1, B, 1, past_len=S + step, want_logits=True)
+        co, lo = o.forward(x1, B, 1, past_len=S + step, want_logits=True)
+        check_logits(lg, lo, "bf16", f"int8 classifier step {step}")
+        assert_ids_match(cg, co, lo, f"int8 classifier step {step}")
