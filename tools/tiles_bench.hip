@@ -1,5 +1,5 @@
 // tools/tiles_bench.hip — batched decode GEMV geometry sweep (round 5).  For each BLOOM block matrix and
-// M = 8 / 32 rows: the library's path (launch_linear_ln / launch_linear: what a decode step runs) and gemv_ldsw4 at every
+// M = 2 / 4 / 8 / 16 / 32 rows: the library's path (launch_linear_ln / launch_linear: what a decode step runs) and gemv_ldsw4 at every
 // (T tiles per block, KS K splits, waves) whose K parts divide K.  The weights rotate over copies totalling > 512 MB so
 // every launch streams from HBM (not the 256 MB Infinity Cache), as in a decode step.  Time = median over 5 groups of
 // (copies) back-to-back launches between HIP events.  Per-CU bytes: the busiest CU's weight + activation bytes.
@@ -42,7 +42,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const char* only = argc > 1 && strcmp(argv[1], "all") ? argv[1] : nullptr;  // tiles_bench [shape filter|all] [M]
-  const int mlist[3] = {8, 16, 32};
+  const int mlist[5] = {2, 4, 8, 16, 32};
   for (int M : mlist) {
     if (argc > 2 && M != atoi(argv[2])) continue;
     for (auto& sh : shapes) {
