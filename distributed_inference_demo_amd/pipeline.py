@@ -35,19 +35,43 @@ class StageExecutor:
     def __init__(self, stage):
         self.stage = stage
         self._sh = None
+        self._side = None
 
     def set_stream(self, handle):
         self._sh = handle
 
+    def _run(self, call, tensors):
+        """Enqueue `call(stream handle)` ordered with torch's current stream.  Torch's default stream has handle 0,
+        which the C-ABI reads as NULL = the stage's own (non-blocking) stream, unordered with it: on the default
+        stream the call runs on a side stream fenced both ways instead."""
+        sh = torch.cuda.current_stream().cuda_stream
+        if sh:
+            call(sh)
+            return
+        cur = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream(cur.device)
+        self._side.wait_stream(cur)
+        call(self._side.cuda_stream)
+        for t in tensors:
+            if t is not None:
+                t.record_stream(self._side)
+        cur.wait_stream(self._side)
+
     def forward(self, inp, out, batch, seq, slot, past_len):
         sh = self._sh if self._sh is not None else torch.cuda.current_stream().cuda_stream
-        self.stage.forward(inp, out, batch, seq, slot=slot, past_len=past_len, stream=sh)
+        if sh:  # the pipeline's rounds: a stream of their own (the host enqueue stays one call)
+            self.stage.forward(inp, out, batch, seq, slot=slot, past_len=past_len, stream=sh)
+            return
+        self._run(lambda h: self.stage.forward(inp, out, batch, seq, slot=slot, past_len=past_len, stream=h),
+                  (inp, out))
 
     def head_norm(self, hidden, batch, seq, xn):
-        self.stage.head_norm(hidden, batch, seq, xn, stream=torch.cuda.current_stream().cuda_stream)
+        self._run(lambda sh: self.stage.head_norm(hidden, batch, seq, xn, stream=sh), (hidden, xn))
 
     def head_slice(self, xn, batch, keys_in, keys_out, tokens):
-        self.stage.head_slice(xn, batch, keys_in, keys_out, tokens, stream=torch.cuda.current_stream().cuda_stream)
+        self._run(lambda sh: self.stage.head_slice(xn, batch, keys_in, keys_out, tokens, stream=sh),
+                  (xn, keys_in, keys_out, tokens))
 
 
 def vocab_slices(vocab, world):

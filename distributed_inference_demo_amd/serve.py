@@ -23,6 +23,10 @@ placement (`placement.stage_ranges`).  Lifecycle:
            The admission schedule depends only on the prompt lengths, so every rank derives the same
            per-row positions and prefill passes;
   finish — rank 0 returns every sample's `max_length` greedy token ids and the run's tokens/s.
+max_length == 0 is the classification task (Communication.java:591-603: one OneStep pass per sample, the
+last device's classifier tail, binaryClassify at Communication.java:532-534): the last stage holds a
+score head of `n_labels` labels (BS_FLAG_CLASSIFIER), samples of equal prompt length go through
+together, `core_pool_size` rows a pass, and rank 0 returns each sample's class id (first maximal label).
 Differences from the reference, by design: full-context decode (the reference
 header feeds only the last token), argmax instead of unseeded top-k, token ids in (no tokenizer).
 
@@ -51,8 +55,9 @@ class RunConfig:
     """The run config of server.py:998-1013 that shapes the computation."""
     model: str = "bloom-560m"
     num_sample: int = 8
-    max_length: int = 40          # tokens generated per sample
+    max_length: int = 40          # tokens generated per sample; 0 = the classification task
     core_pool_size: int = 1       # samples in flight
+    n_labels: int = 2             # classification: score-head labels (the reference's binary classifier)
     prompt_len: int = 16          # synthetic prompts (token ids U[0, V), seed 1234 + sample id)
     dtype: str = "bf16"
     seed: int = 0                 # weight generator seed
@@ -91,8 +96,8 @@ def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory
     lengths (None: synthetic).  Returns {"samples": [[max_length ids] per sample], ...} on rank 0,
     None elsewhere.  Collective: every rank calls it with the same cfg."""
     say = log if (log is not None and rank == 0) else (lambda *_: None)
-    if cfg.num_sample < 1 or cfg.max_length < 1 or cfg.core_pool_size < 1:
-        raise ValueError("num_sample, max_length and core_pool_size must be >= 1")
+    if cfg.num_sample < 1 or cfg.max_length < 0 or cfg.core_pool_size < 1:
+        raise ValueError("num_sample and core_pool_size must be >= 1, max_length >= 0 (0: classification)")
     model = config.get(cfg.model) if isinstance(cfg.model, str) else cfg.model
     if rank == 0:
         prompts = synthetic_prompts(cfg, model.vocab) if prompts is None else [list(p) for p in prompts]
@@ -109,6 +114,8 @@ def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory
             t = t.to(device)
         dist.broadcast(t, src=0)
         lens = [int(v) for v in t.tolist()]
+    if cfg.max_length == 0:
+        return _classify_run(cfg, model, rank, world, device, prompts, lens, executor_factory, say)
     # samples in flight = n_mb micro-batches x mb rows: one micro-batch per stage keeps every stage
     # busy; the rest of the pool rides as rows of a micro-batch (one GPU: one batched decode)
     n_mb = min(cfg.core_pool_size, world)
@@ -193,6 +200,64 @@ def run_rank(cfg: RunConfig, rank, world, device, prompts=None, executor_factory
     res = {"samples": out, "num_sample": cfg.num_sample, "max_length": cfg.max_length,
            "core_pool_size": cfg.core_pool_size, "stages": world, "prompt_lens": lens, "rounds": T,
            "prefill": pf, "seconds": dt, "tokens_per_s": cfg.num_sample * cfg.max_length / dt}
+    say(STATES[2], {k: v for k, v in res.items() if k != "samples"})
+    say(STATES[3], {})
+    return res
+
+
+def classify_batches(lens, rows):
+    """The classification passes: samples grouped by prompt length (a pass is one prompt length for every
+    row, Pipeline.step), in sample order within a group, `rows` samples a pass.  Returns [(length, [sample
+    ids])]; a short last pass of a group is padded by the caller."""
+    groups = {}
+    for i, n in enumerate(lens):
+        groups.setdefault(n, []).append(i)
+    return [(n, ids[k:k + rows]) for n, ids in groups.items() for k in range(0, len(ids), rows)]
+
+
+def _classify_run(cfg, model, rank, world, device, prompts, lens, executor_factory, say):
+    """max_length == 0 (Communication.java:591-603): every sample is one pass through the stages from empty KV
+    rows; the last stage's classifier tail returns its class id."""
+    from .pipeline import classify
+    if cfg.n_labels < 1:
+        raise ValueError("classification needs n_labels >= 1")
+    n_mb = min(cfg.core_pool_size, world)
+    mb = -(-cfg.core_pool_size // n_mb)
+    rows = n_mb * mb
+    passes = classify_batches(lens, rows)
+    pipe, (lb, le) = build_rank(model, rank, world, device, dtype=cfg.dtype, mb_rows=mb, n_mb=n_mb,
+                                max_ctx=max(lens) + 1, max_seq=max(lens), seed=cfg.seed, head_split=False,
+                                executor_factory=executor_factory, n_labels=cfg.n_labels)
+    say(STATES[0], {"rank_layers": [lb, le], "stages": world, "core_pool_size": cfg.core_pool_size,
+                    "micro_batches": n_mb, "rows_per_micro_batch": mb, "passes": len(passes),
+                    "task": "classification", "n_labels": cfg.n_labels})
+    cuda = device.type == "cuda"
+    if cuda:
+        torch.cuda.set_stream(torch.cuda.Stream(device))  # as the generation task (1-token prompts replay graphs)
+    if world > 1:
+        dist.barrier()
+    say(STATES[1], {"num_sample": cfg.num_sample, "max_length": 0})
+    out = [None] * cfg.num_sample
+    t_start = time.perf_counter()
+    for n, ids in passes:
+        prompt = None
+        if rank == 0:  # a short pass repeats its first sample in the spare rows (their classes are dropped)
+            prompt = torch.tensor([prompts[i] for i in ids] + [prompts[ids[0]]] * (rows - len(ids)),
+                                  dtype=torch.int32, device=device)
+        cls = classify(pipe, prompt, n)
+        if rank == 0:
+            for i, c in zip(ids, cls.tolist()):
+                out[i] = int(c)
+    if cuda:
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t_start
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        return None
+    res = {"samples": out, "task": "classification", "n_labels": cfg.n_labels, "num_sample": cfg.num_sample,
+           "max_length": 0, "core_pool_size": cfg.core_pool_size, "stages": world, "prompt_lens": lens,
+           "passes": len(passes), "seconds": dt, "samples_per_s": cfg.num_sample / dt}
     say(STATES[2], {k: v for k, v in res.items() if k != "samples"})
     say(STATES[3], {})
     return res

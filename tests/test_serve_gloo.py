@@ -31,12 +31,31 @@ def _reference(prompts, max_length):
     return out
 
 
-def _worker(rank, world, port, q, head_split):
+def _classes(prompts, n_labels):
+    """Each sample alone through one whole-model classifier stage (the checker)."""
+    out = []
+    for p in prompts:
+        st = OracleStage(MODEL.hidden, MODEL.n_head, MODEL.n_layer, MODEL.vocab, 0, MODEL.n_layer, max_batch=1,
+                         max_ctx=len(p) + 1, seed=SEED, n_labels=n_labels)
+        out.append(int(st.forward(np.array(p, np.int32).reshape(1, -1), 1, len(p))[0]))
+    return out
+
+
+CLS_PROMPTS = [np.random.default_rng(11).integers(0, MODEL.vocab, size=n).tolist() for n in (4, 7, 4, 4, 2, 7, 4)]
+
+
+def _worker(rank, world, port, q, head_split, cls=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        cfg = RunConfig(**{**CFG.__dict__, "head_split": head_split})
-        res = run_rank(cfg, rank, world, torch.device("cpu"), executor_factory=OracleExecutor)
+        if cls:
+            cfg = RunConfig(**{**CFG.__dict__, "num_sample": len(CLS_PROMPTS), "max_length": 0, "n_labels": 3,
+                               "core_pool_size": 3})
+            res = run_rank(cfg, rank, world, torch.device("cpu"), prompts=CLS_PROMPTS if rank == 0 else None,
+                           executor_factory=OracleExecutor)
+        else:
+            cfg = RunConfig(**{**CFG.__dict__, "head_split": head_split})
+            res = run_rank(cfg, rank, world, torch.device("cpu"), executor_factory=OracleExecutor)
         if rank == 0:
             q.put(res)
     finally:
@@ -99,6 +118,37 @@ def test_serve_max_length_one_is_prefill_only():
     cfg = RunConfig(**{**CFG.__dict__, "num_sample": 3, "core_pool_size": 2, "max_length": 1})
     res = run_rank(cfg, 0, 1, torch.device("cpu"), prompts=prompts, executor_factory=OracleExecutor)
     assert res["rounds"] == 0 and res["samples"] == _reference(prompts, 1)
+
+
+def test_serve_classification_single_rank():
+    """max_length = 0 (Communication.java:591-603): one pass per sample through a classifier tail, samples of
+    equal prompt length batched 3 rows a pass (lengths 4, 7, 4, 4, 2, 7, 4 -> passes of 3 + 1 + 2 + 1 rows);
+    every class id equals the checker run on that sample alone."""
+    cfg = RunConfig(**{**CFG.__dict__, "num_sample": len(CLS_PROMPTS), "max_length": 0, "n_labels": 3,
+                       "core_pool_size": 3})
+    res = run_rank(cfg, 0, 1, torch.device("cpu"), prompts=CLS_PROMPTS, executor_factory=OracleExecutor)
+    assert res["task"] == "classification" and res["passes"] == 4
+    assert res["samples"] == _classes(CLS_PROMPTS, 3)
+    from distributed_inference_demo_amd.serve import classify_batches
+    assert classify_batches([4, 7, 4, 4, 2, 7, 4], 3) == [(4, [0, 2, 3]), (4, [6]), (7, [1, 5]), (2, [4])]
+    with pytest.raises(ValueError):
+        run_rank(RunConfig(**{**cfg.__dict__, "max_length": -1}), 0, 1, torch.device("cpu"), prompts=CLS_PROMPTS,
+                 executor_factory=OracleExecutor)
+
+
+def test_serve_classification_two_ranks():
+    """The same task over 2 gloo ranks: layers split, the classifier on rank 1, class ids back to rank 0."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, False, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res["stages"] == 2 and res["samples"] == _classes(CLS_PROMPTS, 3)
 
 
 def test_serve_rejects_empty_prompts():
