@@ -67,10 +67,18 @@ class StageExecutor:
                   (inp, out))
 
     def head_norm(self, hidden, batch, seq, xn):
-        self._run(lambda sh: self.stage.head_norm(hidden, batch, seq, xn, stream=sh), (hidden, xn))
+        sh = torch.cuda.current_stream().cuda_stream
+        if sh:
+            self.stage.head_norm(hidden, batch, seq, xn, stream=sh)
+            return
+        self._run(lambda h: self.stage.head_norm(hidden, batch, seq, xn, stream=h), (hidden, xn))
 
     def head_slice(self, xn, batch, keys_in, keys_out, tokens):
-        self._run(lambda sh: self.stage.head_slice(xn, batch, keys_in, keys_out, tokens, stream=sh),
+        sh = torch.cuda.current_stream().cuda_stream
+        if sh:
+            self.stage.head_slice(xn, batch, keys_in, keys_out, tokens, stream=sh)
+            return
+        self._run(lambda h: self.stage.head_slice(xn, batch, keys_in, keys_out, tokens, stream=h),
                   (xn, keys_in, keys_out, tokens))
 
 
