@@ -187,3 +187,32 @@ def test_bloom1b1_full_bf16_against_fp32_reference():
     assert rec["first_divergence_step"] is None, rec
     assert max(rec["tf_max"]) <= FP32REF_MAX_TOL, rec["tf_max"]
     assert max(rec["tf_mean"]) <= FP32REF_MEAN_TOL, rec["tf_mean"]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_bloom560m_full_depth_classification_two_stages(dtype):
+    """The classification task at a real configuration: bloom-560m, all 24 layers, split as the server would place it
+    on two devices (header [0, 12) -> classifier tail [12, 24), n_labels = 2: run_inference_master_residual ->
+    run_inference_worker_residual_last_classification, inference.cpp:220-270), 3 samples x 24 tokens.  Pooled logits
+    against the checker in the same mode (fp32: relative 1e-3; bf16: the flat 2e-2) and the class ids equal unless the
+    checker's own margin is inside that bound."""
+    from test_gpu_parity import check_logits
+    m = config.get("bloom-560m")
+    B, P, half = 3, 24, m.n_layer // 2
+    tw = dtype == "bf16"
+    head = Stage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, half, dtype=dtype, max_batch=B, max_ctx=P,
+                 max_tokens=B * P, seed=7, is_last=False)
+    tail = Stage(m.hidden, m.n_head, m.n_layer, m.vocab, half, m.n_layer, dtype=dtype, max_batch=B, max_ctx=P,
+                 max_tokens=B * P, seed=7, n_labels=2)
+    o = OracleStage(m.hidden, m.n_head, m.n_layer, m.vocab, 0, m.n_layer, bf16=tw, max_batch=B, max_ctx=P, seed=7,
+                    n_labels=2)
+    ids = prompt_ids(4321, B, P, m.vocab)
+    hid = head.forward_host(ids, B, P)
+    cg, lg = tail.forward_host(hid, B, P, want_logits=True)
+    co, lo = o.forward(ids, B, P, want_logits=True)
+    assert lg.shape == (B, 2)
+    check_logits(lg, lo, dtype, f"bloom-560m classifier {dtype}")
+    assert_ids_match(cg, co, lo, f"bloom-560m classifier {dtype}",
+                     tol=2e-2 if tw else 1e-3 * float(np.abs(lo).max()))
+    for s in (head, tail, o):
+        s.close()
