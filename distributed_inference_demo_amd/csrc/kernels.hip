@@ -1485,12 +1485,30 @@ static bool tiles_take(int M, int K) {
   return M >= 3 || (M == 2 && K >= 2560);
 }
 
+// Largest token count of the batched tile GEMV: 64 (bf16 weights, four m-tiles, 32 < M <= 64: short prefills, which
+// the prefill GEMMs' 128-row tiles serve with most of each tile and most CUs idle), or 32 with BS_TILES_MAX_M=32
+// (A/B knob, read once).
+static int tiles_max_m() {
+  static const int v = [] {
+    const char* e = getenv("BS_TILES_MAX_M");
+    return e && atoi(e) == 32 ? 32 : 64;
+  }();
+  return v;
+}
+
 // ln != nullptr (bf16): X = LN(ln->x) fused into gemv_ldsw4's prologue when the shape takes one K split of
 // 2..5 stages per wave and M <= 16; otherwise returns false and the caller normalises first.
+// 32 < M <= 64 (bf16, no LN): gemv_ldsw4 with four m-tiles where the table's tile count is <= 3 (the LDS of the wave
+// partials), else false (the prefill GEMM).
 template <typename WT = bf16>
 static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K, const Epi& ep, hipStream_t s,
                                 const LnArgs* ln = nullptr) {
-  if (!tiles_take(M, K) || M > 32 || (K % 64) != 0) return false;
+  if (!tiles_take(M, K) || M > 64 || (K % 64) != 0) return false;
+  const bool four = M > 32;
+  // four m-tiles only on the long-K shapes (fc2, K = 4N), whose prefill GEMM has few output tiles: bloom-1b1 fc2 at 64
+  // tokens 22.4 -> 18.1 us, while QKV / fc1 (10.8 / 9.2 -> 12.2 us) and dense (8.3 -> 9.6 us) keep the GEMM's
+  // 64 x 32 tiles (profiles/r06_tiles_four_m_ab.txt)
+  if (four && (sizeof(WT) != 2 || ln || M > tiles_max_m() || K < 4 * N)) return false;
   const int units = K / 64;
   int T = N >= 16384 ? 4 : 2, KS = 1, WV = 0;
   for (const TileCfg& c : kTileTable)
@@ -1521,9 +1539,16 @@ static bool gemv_tiles_dispatch(const bf16* x, const WT* w, int M, int N, int K,
       }
       return false;
     }
+    if (four && (T > 3 || K % (KS * 8 * KC) != 0)) return false;
     if (T <= 4 && K % (KS * 8 * KC) == 0) {
       auto go4 = [&](auto tc) {
         constexpr int TT = decltype(tc)::value;
+        if constexpr (TT <= 3 && sizeof(WT) == 2) {
+          if (four) {
+            gemv_ldsw4_launch<TT, 8, 4, WT>(x, w, M, N, K, KS, ep, s);
+            return;
+          }
+        }
         if (two) gemv_ldsw4_launch<TT, 8, 2, WT>(x, w, M, N, K, KS, ep, s);
         else gemv_ldsw4_launch<TT, 8, 1, WT>(x, w, M, N, K, KS, ep, s);
       };
@@ -2551,6 +2576,7 @@ void launch_linear(int is_bf16, const void* X, const void* W, int M, int N, int 
     gemv_dispatch<false>(x, LnArgs{}, w, M, N, K, ep, s);
     return;
   }
+  if (M <= 64 && gemv_tiles_dispatch(x, w, M, N, K, ep, s)) return;
   if ((K % 64) == 0) {
     // 128x128 when it still gives every CU a block (>= 240 blocks), else 64x64, else 64x32
     auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };

@@ -137,3 +137,27 @@ def test_two_to_four_rows_decode_split_attention(h, nh, B):
                     f"h={h} B={B} decode step {step}")
     gs.close()
     os_.close()
+
+
+@pytest.mark.parametrize("h,nh", [(1024, 16), (1536, 16), (2560, 32), (4096, 32)])
+@pytest.mark.parametrize("B,S", [(3, 11), (2, 24), (1, 64), (4, 16)])
+def test_short_prefill_four_m_tiles(h, nh, B, S):
+    """33 <= B x S <= 64 tokens (a short prefill): fc2 (K = 4N) on the batched tile GEMV with four m-tiles (round 6;
+    before, the prefill GEMM), split-K at bloom-1b1 / 3b / 7b1 widths; QKV / dense / fc1 on the prefill GEMMs.  Ragged
+    row counts (33, 48), one row of 64 tokens, 4 rows of 16.  A 2-layer middle stage at a slot offset, then 2 decode
+    steps of the same rows."""
+    from test_gpu_parity import check_close as _cc
+    check_close = (lambda g, o, dt, what: check_h4096_hidden(g, o, what)) if h == 4096 else _cc
+    L, V = 3, 1024
+    gs, os_ = pair(h, nh, L, V, 1, 3, "bf16", seed=47, max_batch=B + 1, max_ctx=S + 4, max_tokens=B * S,
+                   is_first=False, is_last=False)
+    rng = np.random.default_rng(13)
+    x = (2.0 + rng.standard_normal((B, S, h))).astype(np.float32)
+    check_close(gs.forward_host(x, B, S, slot=1, past_len=0), os_.forward(x, B, S, slot=1, past_len=0), "bf16",
+                f"h={h} B={B} S={S} prefill")
+    for step in range(2):
+        x1 = (2.0 + rng.standard_normal((B, 1, h))).astype(np.float32)
+        check_close(gs.forward_host(x1, B, 1, slot=1, past_len=S + step),
+                    os_.forward(x1, B, 1, slot=1, past_len=S + step), "bf16", f"h={h} B={B} S={S} decode step {step}")
+    gs.close()
+    os_.close()
